@@ -1,0 +1,104 @@
+/*
+ * qce.h — C ABI of the MI355X-native Bussgang-GMM channel estimator (libqce.so).
+ *
+ * This is the drop-in boundary for the hot path of benediktfesl/Quantized_Channel_Estimation:
+ * the per-SNR precompute and the per-batch estimate of `Gmm_nbit` (modules/gmm_cplx_bussgang.py)
+ * and its twin `Gmm_quant` (modules/gmm_cplx_quant.py:190-457).  The Python host class
+ * `quantized_channel_estimation_amd.Gmm_nbit` binds these entry points through ctypes
+ * (INTEGRATION.md shows the binding a maintainer of the reference would add).
+ *
+ * Conventions
+ *  - complex numbers are interleaved (re, im) doubles, numpy complex128 layout; all arrays are
+ *    row-major (C order) and contiguous;
+ *  - `io` selects where the caller's I/O buffers live: QCE_IO_HOST (host memory, the call is
+ *    synchronous) or QCE_IO_DEVICE (device memory of the model's device, e.g. a torch tensor's
+ *    data_ptr(); the call is asynchronous on `stream`, NULL = the model's own stream);
+ *  - the library owns the per-model device tables; a model is bound to one device and is not
+ *    thread-safe (use one model per thread/stream);
+ *  - every entry point returns a status code (QCE_OK = 0); `qce_last_error()` returns the message
+ *    of the last failure on the calling thread.  No C++ exception crosses the ABI.
+ */
+#ifndef QCE_H
+#define QCE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct qce_model qce_model;
+
+/* status codes */
+#define QCE_OK 0
+#define QCE_EARG 1     /* invalid argument (shape, pointer, mode)            -> ValueError          */
+#define QCE_ECHOL 2    /* Cr_k not positive definite (gmm_cplx_bussgang.py:43-46) -> ValueError      */
+#define QCE_ENOTIMPL 3 /* configuration the kernels do not cover          -> NotImplementedError */
+#define QCE_EHIP 4     /* HIP runtime failure                              -> RuntimeError        */
+#define QCE_ESTATE 5   /* call order (estimate before prepare)             -> RuntimeError        */
+
+/* estimate modes (gmm_cplx_bussgang.py:197-242) */
+#define QCE_MODE_ALL 0  /* 'all': sum of all responsibility-weighted LMMSE estimates   (:220-228) */
+#define QCE_MODE_TOPN 1 /* int n: top-n by responsibility, renormalised; n == 1 -> argmax (:197-219) */
+#define QCE_MODE_CUMP 2 /* float p: shortest descending prefix with cumulative prob >= p (:229-242) */
+
+/* quantiser kinds for multi-bit n_bits (gmm_cplx_bussgang.py:281-284) */
+#define QCE_QUANT_UNIFORM 0
+#define QCE_QUANT_LLOYD 1
+#define QCE_QUANT_OTHER 2 /* any other string: the reference leaves the Bussgang gain at 0 */
+
+#define QCE_IO_HOST 0
+#define QCE_IO_DEVICE 1
+
+int qce_version(void);
+const char* qce_last_error(void);
+int qce_device_count(int* count);
+
+/* Model parameters after `Gmm_nbit.fit` (gmm_cplx_bussgang.py:96-163): means_cplx (K,N) c128,
+ * covs_cplx (K,N,N) c128, gm.weights_ (K,) f64.  Replaces the attribute bag the reference keeps in
+ * its sklearn GaussianMixture (:86-94).  N <= 64 (padded internally to 16/32/64), K <= 256 for the
+ * selective modes. */
+int qce_model_create(int K, int N, const double* means_cplx, const double* covs_cplx, const double* weights,
+                     int device, qce_model** out);
+int qce_model_destroy(qce_model* model);
+
+/* Per-SNR precompute: `_prepare_for_prediction` (gmm_cplx_bussgang.py:246-328).
+ * A: (M,N) c128 observation matrix, or NULL for the identity (estimate_from_y :191-192).
+ * n_bits: 1..8 or +INFINITY (np.inf).  thresholds (2^b-1) / labels (2^b) are the quantiser
+ * tables of the lloyd kind (lloyd_max_quantizer.py:24-37); NULL otherwise.
+ * Returns QCE_ECHOL if some Cr_k is not positive definite (:43-46). */
+int qce_prepare(qce_model* model, const double* A, int M, double snr_db, double n_bits, int quant_kind,
+                const double* thresholds, const double* labels, int n_levels);
+
+/* Channel estimates: `estimate_from_y` (gmm_cplx_bussgang.py:166-243) for y (B,M) c128 -> h (B,N) c128.
+ * mode/mode_param: QCE_MODE_ALL; QCE_MODE_TOPN with n; QCE_MODE_CUMP with p. */
+int qce_estimate(qce_model* model, const double* y, int64_t B, int mode, double mode_param, double* h_out, int io,
+                 void* stream);
+
+/* `_estimate_weighted_log_prob` (:369-386) -> lp (B,K) f64; `predict_proba_cplx` (:351-367) -> proba (B,K);
+ * `_predict_cplx` (:335-349) -> labels (B,) int64.  Any output pointer may be NULL. */
+int qce_log_prob(qce_model* model, const double* X, int64_t B, double* lp_out, double* proba_out,
+                 int64_t* labels_out, int io, void* stream);
+
+/* K-shard partial of the 'all' mode for the components this model holds: per sample the running max
+ * m (B,) f64, the sum s = sum_k exp(lp_k - m) (B,) f64 and acc = sum_k exp(lp_k - m) (W_k y + b_k)
+ * (B, 2N) f32 interleaved; h = (sum_g acc_g e^{m_g}) / (sum_g s_g e^{m_g}). */
+int qce_estimate_partial(qce_model* model, const double* y, int64_t B, double* m_out, double* s_out, float* acc_out,
+                         int io, void* stream);
+
+/* Per-SNR tables for state mirroring (the reference mutates gm.means_, gm.covariances_,
+ * gm.precisions_cholesky_, :262-313) and tests.  Host pointers, any may be NULL:
+ * means_y (K,M), Cy (K,M,M), Cr (K,M,M), P (K,M,M) = (L^-1)^H, A_eff (K,M,N), W (K,N,M),
+ * b (K,N), cconst (K,) = -M log(pi) + 2 log det P_k + log w_k. */
+int qce_get_tables(qce_model* model, double* means_y, double* Cy, double* Cr, double* P, double* A_eff, double* W,
+                   double* b, double* cconst);
+
+/* Dimensions of the prepared state: M (0 before the first prepare). */
+int qce_model_info(qce_model* model, int* K, int* N, int* M, int* device);
+
+/* Device synchronisation of the model's stream (for timing and for QCE_IO_DEVICE callers). */
+int qce_synchronize(qce_model* model);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QCE_H */

@@ -1,0 +1,207 @@
+"""ctypes binding of libqce.so (include/qce.h).
+
+The library is the only compute path: if it is missing or no HIP device is visible, every
+estimator call raises — there is no CPU fallback in this package.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libqce.so")
+
+QCE_OK, QCE_EARG, QCE_ECHOL, QCE_ENOTIMPL, QCE_EHIP, QCE_ESTATE = range(6)
+MODE_ALL, MODE_TOPN, MODE_CUMP = 0, 1, 2
+QUANT_UNIFORM, QUANT_LLOYD, QUANT_OTHER = 0, 1, 2
+IO_HOST, IO_DEVICE = 0, 1
+
+_c_dbl_p = ctypes.POINTER(ctypes.c_double)
+_c_flt_p = ctypes.POINTER(ctypes.c_float)
+_c_i64_p = ctypes.POINTER(ctypes.c_int64)
+_vp = ctypes.c_void_p
+
+# name -> (restype, argtypes); every symbol include/qce.h declares
+SIGNATURES = {
+    "qce_version": (ctypes.c_int, []),
+    "qce_last_error": (ctypes.c_char_p, []),
+    "qce_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "qce_model_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, ctypes.c_int,
+                                        ctypes.POINTER(_vp)]),
+    "qce_model_destroy": (ctypes.c_int, [_vp]),
+    "qce_prepare": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int, _vp, _vp,
+                                   ctypes.c_int]),
+    "qce_estimate": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, _vp, ctypes.c_int, _vp]),
+    "qce_log_prob": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int, _vp]),
+    "qce_estimate_partial": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int, _vp]),
+    "qce_get_tables": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "qce_model_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                      ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "qce_synchronize": (ctypes.c_int, [_vp]),
+}
+
+_lib = None
+
+
+class QceError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libqce.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: build it with `python -m quantized_channel_estimation_amd.build`"
+                          " (there is no CPU fallback)")
+    # One HIP runtime per process: torch ships its own libamdhip64 (SONAME libamdhip64.so.7, loaded
+    # from torch/lib as "libamdhip64.so").  Loading torch first makes libqce.so's NEEDED
+    # libamdhip64.so.7 bind to that same runtime; the other order leaves two HIP/HSA runtimes in
+    # the process and torch then reports no GPU.
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is part of the image
+        pass
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    """Map a status code to the reference's exception types."""
+    if rc == QCE_OK:
+        return
+    msg = load().qce_last_error().decode("utf-8", "replace")
+    if rc in (QCE_EARG, QCE_ECHOL):
+        raise ValueError(msg)
+    if rc == QCE_ENOTIMPL:
+        raise NotImplementedError(msg)
+    raise QceError(f"[qce status {rc}] {msg}")
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    check(load().qce_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def ptr(a):
+    """Data pointer of a contiguous numpy array or torch tensor (None -> NULL)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        if not a.flags["C_CONTIGUOUS"]:
+            raise ValueError("array must be C-contiguous")
+        return a.ctypes.data
+    return a.data_ptr()
+
+
+class DeviceModel:
+    """Owner of one qce_model handle (device tables of one Gaussian mixture on one GPU)."""
+
+    def __init__(self, means_cplx, covs_cplx, weights, device=0):
+        lib = load()
+        covs = np.ascontiguousarray(covs_cplx, dtype=np.complex128)
+        K, N = covs.shape[0], covs.shape[-1]
+        means = None if means_cplx is None else np.ascontiguousarray(means_cplx, dtype=np.complex128).reshape(K, N)
+        w = np.ascontiguousarray(weights, dtype=np.float64).reshape(K)
+        h = _vp()
+        check(lib.qce_model_create(K, N, ptr(means), ptr(covs), ptr(w), int(device), ctypes.byref(h)))
+        self._h = h
+        self.K, self.N, self.device = K, N, int(device)
+        self.M = 0
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().qce_model_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def prepare(self, A, snr_db, n_bits, quant_kind=QUANT_UNIFORM, thresholds=None, labels=None):
+        lib = load()
+        if A is None:
+            M, a = self.N, None
+        else:
+            a = np.ascontiguousarray(A, dtype=np.complex128)
+            if a.ndim != 2 or a.shape[1] != self.N:
+                raise ValueError(f"A must be (M, {self.N}), got {a.shape}")
+            M = a.shape[0]
+        thr = lab = None
+        nlev = 0
+        if labels is not None:
+            lab = np.ascontiguousarray(labels, dtype=np.float64)
+            thr = np.ascontiguousarray(thresholds, dtype=np.float64)
+            nlev = lab.size
+        check(lib.qce_prepare(self._h, ptr(a), int(M), float(snr_db), float(n_bits), int(quant_kind), ptr(thr),
+                              ptr(lab), int(nlev)))
+        self.M = M
+
+    def estimate(self, y, mode=MODE_ALL, param=0.0, out=None, stream=None):
+        """y: (B,M) complex128 numpy array (host) or torch.complex128 CUDA tensor (device)."""
+        io = IO_HOST if isinstance(y, np.ndarray) else IO_DEVICE
+        B = y.shape[0]
+        if io == IO_HOST:
+            y = np.ascontiguousarray(y, dtype=np.complex128)
+            if out is None:
+                out = np.empty((B, self.N), dtype=np.complex128)
+        elif out is None:
+            import torch
+            out = torch.empty((B, self.N), dtype=torch.complex128, device=y.device)
+        if y.shape[1] != self.M:
+            raise ValueError(f"y must have {self.M} columns, got {y.shape[1]}")
+        check(load().qce_estimate(self._h, ptr(y), int(B), int(mode), float(param), ptr(out), io, stream))
+        return out
+
+    def log_prob(self, X, want_lp=True, want_proba=False, want_labels=False):
+        X = np.ascontiguousarray(X, dtype=np.complex128)
+        B = X.shape[0]
+        if X.ndim != 2 or X.shape[1] != self.M:
+            raise ValueError(f"X must be (B, {self.M}), got {X.shape}")
+        lp = np.empty((B, self.K)) if want_lp else None
+        pr = np.empty((B, self.K)) if want_proba else None
+        lb = np.empty(B, dtype=np.int64) if want_labels else None
+        check(load().qce_log_prob(self._h, ptr(X), int(B), ptr(lp), ptr(pr), ptr(lb), IO_HOST, None))
+        return lp, pr, lb
+
+    def partial(self, y, m_out=None, s_out=None, acc_out=None, stream=None):
+        io = IO_HOST if isinstance(y, np.ndarray) else IO_DEVICE
+        B = y.shape[0]
+        if io == IO_HOST:
+            y = np.ascontiguousarray(y, dtype=np.complex128)
+            m_out = np.empty(B) if m_out is None else m_out
+            s_out = np.empty(B) if s_out is None else s_out
+            acc_out = np.empty((B, 2 * self.N), dtype=np.float32) if acc_out is None else acc_out
+        else:
+            import torch
+            dev = y.device
+            m_out = torch.empty(B, dtype=torch.float64, device=dev) if m_out is None else m_out
+            s_out = torch.empty(B, dtype=torch.float64, device=dev) if s_out is None else s_out
+            acc_out = torch.empty((B, 2 * self.N), dtype=torch.float32, device=dev) if acc_out is None else acc_out
+        check(load().qce_estimate_partial(self._h, ptr(y), int(B), ptr(m_out), ptr(s_out), ptr(acc_out), io, stream))
+        return m_out, s_out, acc_out
+
+    def tables(self):
+        K, M, N = self.K, self.M, self.N
+        t = dict(means_y=np.empty((K, M), complex), Cy=np.empty((K, M, M), complex), Cr=np.empty((K, M, M), complex),
+                 P=np.empty((K, M, M), complex), A_eff=np.empty((K, M, N), complex), W=np.empty((K, N, M), complex),
+                 b=np.empty((K, N), complex), cconst=np.empty(K))
+        check(load().qce_get_tables(self._h, *(ptr(t[k]) for k in ("means_y", "Cy", "Cr", "P", "A_eff", "W", "b",
+                                                                    "cconst"))))
+        return t
+
+    def synchronize(self):
+        check(load().qce_synchronize(self._h))

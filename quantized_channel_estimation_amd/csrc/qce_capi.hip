@@ -1,0 +1,517 @@
+// C ABI of libqce.so (declared in include/qce.h): model lifetime, per-SNR prepare and the
+// estimate entry points, orchestrating the kernels of qce_prepare.hip / qce_estimate.hip on one
+// HIP stream per model.
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/qce.h"
+#include "qce_common.h"
+#include "qce_kernels.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                               \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess)                                                                          \
+      return fail(QCE_EHIP, std::string(#expr) + " failed: " + hipGetErrorString(e_));             \
+  } while (0)
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc(&p, sizeof(T) * (count ? count : 1));
+    if (e == hipSuccess) n = count;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+int pad_dim(int v) {
+  if (v <= 16) return 16;
+  if (v <= 32) return 32;
+  if (v <= 64) return 64;
+  return -1;
+}
+
+}  // namespace
+
+struct qce_model {
+  int K = 0, N = 0, device = 0;
+  hipStream_t stream = nullptr;
+  int has_mean = 0;
+  std::vector<double> weights;
+  DevBuf<double2> means, covs;
+  DevBuf<double> logw;
+  // prepared state
+  int M = 0, MP = 0, NP = 0, prepared = 0;
+  DevBuf<double2> A, Cy, Cr, Lw, Linv, Aeff, work, V, W, means_y, q0, bvec;
+  DevBuf<double> gain, cconst, thr, lab;
+  DevBuf<int> status;
+  DevBuf<float> pack32;
+  DevBuf<double> pack64;
+  long long stride32 = 0, stride64 = 0;
+  // estimate scratch
+  DevBuf<double2> y_scr, h_scr;
+  DevBuf<double> lp_scr, proba_scr, m_scr, s_scr;
+  DevBuf<float> w_scr, acc_scr;
+  DevBuf<long long> lab_scr;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+hipStream_t pick_stream(qce_model* m, void* stream) { return stream ? (hipStream_t)stream : m->stream; }
+
+QceEstArgs est_args(qce_model* m, const double2* y, long long B) {
+  QceEstArgs a;
+  a.B = B;
+  a.M = m->M;
+  a.N = m->N;
+  a.K = m->K;
+  a.MP = m->MP;
+  a.NP = m->NP;
+  a.has_mean = m->has_mean;
+  a.y = y;
+  a.pack32 = m->pack32.p;
+  a.stride32 = m->stride32;
+  a.pack64 = m->pack64.p;
+  a.stride64 = m->stride64;
+  a.cconst = m->cconst.p;
+  return a;
+}
+
+// stage host input (io == HOST) or use the device pointer directly
+int stage_input(qce_model* m, const double* y, long long B, int io, hipStream_t st, const double2** dy) {
+  if (io == QCE_IO_DEVICE) {
+    *dy = reinterpret_cast<const double2*>(y);
+    return QCE_OK;
+  }
+  HIPCHK(m->y_scr.ensure((size_t)B * m->M));
+  HIPCHK(hipMemcpyAsync(m->y_scr.p, y, sizeof(double2) * (size_t)B * m->M, hipMemcpyHostToDevice, st));
+  *dy = m->y_scr.p;
+  return QCE_OK;
+}
+
+int check_model(qce_model* m, bool need_prepared) {
+  if (!m) return fail(QCE_EARG, "null model");
+  if (need_prepared && !m->prepared) return fail(QCE_ESTATE, "qce_prepare has not been called on this model");
+  return QCE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qce_version(void) { return 100; }
+
+const char* qce_last_error(void) { return g_err.c_str(); }
+
+int qce_device_count(int* count) {
+  if (!count) return fail(QCE_EARG, "null count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *count = n;
+  return QCE_OK;
+}
+
+int qce_model_create(int K, int N, const double* means_cplx, const double* covs_cplx, const double* weights,
+                     int device, qce_model** out) {
+  if (!out || !covs_cplx || !weights) return fail(QCE_EARG, "null argument");
+  *out = nullptr;
+  if (K <= 0 || N <= 0) return fail(QCE_EARG, "K and N must be positive");
+  if (pad_dim(N) < 0) return fail(QCE_ENOTIMPL, "N > 64 is not covered by the estimate kernels yet");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(QCE_EHIP, "no HIP device visible");
+  if (device < 0 || device >= ndev) return fail(QCE_EARG, "device index out of range");
+  DeviceGuard g(device);
+  qce_model* m = new qce_model();
+  m->K = K;
+  m->N = N;
+  m->device = device;
+  m->weights.assign(weights, weights + K);
+  std::vector<double> logw(K);
+  for (int k = 0; k < K; ++k) logw[k] = log(weights[k]);
+  std::vector<double> mz((size_t)2 * K * N, 0.0);
+  if (means_cplx) {
+    memcpy(mz.data(), means_cplx, sizeof(double) * 2 * (size_t)K * N);
+    for (double v : mz)
+      if (v != 0.0) {
+        m->has_mean = 1;
+        break;
+      }
+  }
+  hipError_t e = hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = m->means.ensure((size_t)K * N);
+  if (e == hipSuccess) e = m->covs.ensure((size_t)K * N * N);
+  if (e == hipSuccess) e = m->logw.ensure(K);
+  if (e == hipSuccess) e = hipMemcpy(m->means.p, mz.data(), sizeof(double2) * (size_t)K * N, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = hipMemcpy(m->covs.p, covs_cplx, sizeof(double2) * (size_t)K * N * N, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(m->logw.p, logw.data(), sizeof(double) * K, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    qce_model_destroy(m);
+    return fail(QCE_EHIP, std::string("model allocation failed: ") + hipGetErrorString(e));
+  }
+  *out = m;
+  return QCE_OK;
+}
+
+int qce_model_destroy(qce_model* m) {
+  if (!m) return QCE_OK;
+  DeviceGuard g(m->device);
+  if (m->stream) (void)hipStreamSynchronize(m->stream);
+  for (auto* b : {&m->means, &m->covs, &m->A, &m->Cy, &m->Cr, &m->Lw, &m->Linv, &m->Aeff, &m->work, &m->V, &m->W,
+                  &m->means_y, &m->q0, &m->bvec, &m->y_scr, &m->h_scr})
+    b->release();
+  for (auto* b : {&m->logw, &m->gain, &m->cconst, &m->thr, &m->lab, &m->pack64, &m->lp_scr, &m->proba_scr,
+                  &m->m_scr, &m->s_scr})
+    b->release();
+  m->status.release();
+  m->pack32.release();
+  m->w_scr.release();
+  m->acc_scr.release();
+  m->lab_scr.release();
+  if (m->stream) (void)hipStreamDestroy(m->stream);
+  delete m;
+  return QCE_OK;
+}
+
+int qce_prepare(qce_model* m, const double* A, int M, double snr_db, double n_bits, int quant_kind,
+                const double* thresholds, const double* labels, int n_levels) {
+  int rc = check_model(m, false);
+  if (rc) return rc;
+  const int N = m->N, K = m->K;
+  if (!A) M = N;
+  if (M <= 0) return fail(QCE_EARG, "M must be positive");
+  if (pad_dim(M) < 0) return fail(QCE_ENOTIMPL, "M > 64 is not covered by the estimate kernels yet");
+  int kind;
+  int nb = 0;
+  if (n_bits == 1.0) {
+    kind = 0;
+  } else if (isinf(n_bits) && n_bits > 0) {
+    kind = 2;
+  } else {
+    if (!(n_bits >= 2.0 && n_bits <= 8.0) || n_bits != floor(n_bits))
+      return fail(QCE_ENOTIMPL, "n_bits must be 1..8 or inf");
+    kind = 1;
+    nb = (int)n_bits;
+  }
+  if (kind == 1 && quant_kind == QCE_QUANT_LLOYD) {
+    if (!thresholds || !labels || n_levels != (1 << nb))
+      return fail(QCE_EARG, "lloyd quantiser needs 2^b labels and 2^b-1 thresholds");
+  }
+  DeviceGuard g(m->device);
+  hipStream_t st = m->stream;
+  const size_t KMM = (size_t)K * M * M, KMN = (size_t)K * M * N;
+  HIPCHK(m->A.ensure((size_t)M * N));
+  HIPCHK(m->Cy.ensure(KMM));
+  HIPCHK(m->Cr.ensure(KMM));
+  HIPCHK(m->Lw.ensure(KMM));
+  HIPCHK(m->Linv.ensure(KMM));
+  HIPCHK(m->Aeff.ensure(KMN));
+  HIPCHK(m->work.ensure(KMN));
+  HIPCHK(m->V.ensure(KMN));
+  HIPCHK(m->W.ensure(KMN));
+  HIPCHK(m->means_y.ensure((size_t)K * M));
+  HIPCHK(m->q0.ensure((size_t)K * M));
+  HIPCHK(m->bvec.ensure((size_t)K * N));
+  HIPCHK(m->gain.ensure((size_t)K * M));
+  HIPCHK(m->cconst.ensure(K));
+  HIPCHK(m->status.ensure(K));
+  HIPCHK(m->thr.ensure(256));
+  HIPCHK(m->lab.ensure(256));
+  const int MP = pad_dim(M), NP = pad_dim(N);
+  const long long s32 = qce_pack_f32_stride(MP, NP, m->has_mean);
+  const long long s64 = qce_pack_f64_stride(MP, m->has_mean);
+  HIPCHK(m->pack32.ensure((size_t)s32 * K));
+  HIPCHK(m->pack64.ensure((size_t)s64 * K));
+  int identityA = 0;
+  if (A) {
+    HIPCHK(hipMemcpyAsync(m->A.p, A, sizeof(double2) * (size_t)M * N, hipMemcpyHostToDevice, st));
+  } else {
+    std::vector<double> eye((size_t)2 * N * N, 0.0);
+    for (int i = 0; i < N; ++i) eye[(size_t)2 * (i * N + i)] = 1.0;
+    HIPCHK(hipMemcpyAsync(m->A.p, eye.data(), sizeof(double2) * (size_t)N * N, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    identityA = 1;
+  }
+  if (A && M == N) {  // an explicit identity takes the same fast path (bitwise the same Cy)
+    identityA = 1;
+    for (int i = 0; i < M && identityA; ++i)
+      for (int j = 0; j < N; ++j) {
+        double re = A[2 * ((size_t)i * N + j)], im = A[2 * ((size_t)i * N + j) + 1];
+        if (im != 0.0 || re != (i == j ? 1.0 : 0.0)) {
+          identityA = 0;
+          break;
+        }
+      }
+  }
+  double delta = 0.0;
+  if (kind == 1 && quant_kind == QCE_QUANT_UNIFORM) {
+    // uniform_quantizer.py:6-23, 44-45
+    static const double tbl[9] = {0, 1.596, 0.9957, 0.5860, 0.3352, 0.1881, 0.1041, 0.0569, 0.0308};
+    delta = sqrt((1.0 + pow(10.0, -snr_db / 10.0)) / 2.0) * tbl[nb];
+  }
+  if (kind == 1 && quant_kind == QCE_QUANT_LLOYD) {
+    HIPCHK(hipMemcpyAsync(m->thr.p, thresholds, sizeof(double) * (n_levels - 1), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(m->lab.p, labels, sizeof(double) * n_levels, hipMemcpyHostToDevice, st));
+  }
+  QcePrepareArgs p;
+  p.K = K;
+  p.N = N;
+  p.M = M;
+  p.MP = MP;
+  p.NP = NP;
+  p.has_mean = m->has_mean;
+  p.identityA = identityA;
+  p.kind = kind;
+  p.n_bits = nb;
+  p.quant_kind = quant_kind;
+  p.sigma2 = pow(10.0, -snr_db / 10.0);
+  p.delta = delta;
+  p.thr = m->thr.p;
+  p.lab = m->lab.p;
+  p.A = m->A.p;
+  p.covs = m->covs.p;
+  p.means = m->means.p;
+  p.logw = m->logw.p;
+  p.Cy = m->Cy.p;
+  p.Cr = m->Cr.p;
+  p.Lw = m->Lw.p;
+  p.Linv = m->Linv.p;
+  p.Aeff = m->Aeff.p;
+  p.work = m->work.p;
+  p.V = m->V.p;
+  p.W = m->W.p;
+  p.means_y = m->means_y.p;
+  p.q0 = m->q0.p;
+  p.bvec = m->bvec.p;
+  p.gain = m->gain.p;
+  p.cconst = m->cconst.p;
+  p.status = m->status.p;
+  p.pack32 = m->pack32.p;
+  p.stride32 = s32;
+  p.pack64 = m->pack64.p;
+  p.stride64 = s64;
+  HIPCHK(qce_launch_prepare(p, st));
+  std::vector<int> status(K);
+  HIPCHK(hipMemcpyAsync(status.data(), m->status.p, sizeof(int) * K, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  m->M = M;
+  m->MP = MP;
+  m->NP = NP;
+  m->stride32 = s32;
+  m->stride64 = s64;
+  for (int k = 0; k < K; ++k)
+    if (status[k]) {
+      m->prepared = 0;
+      return fail(QCE_ECHOL,
+                  "Fitting the mixture model failed because some components have ill-defined empirical covariance "
+                  "(for instance caused by singleton or collapsed samples). Try to decrease the number of "
+                  "components, or increase reg_covar.");
+    }
+  m->prepared = 1;
+  return QCE_OK;
+}
+
+int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode_param, double* h_out, int io,
+                 void* stream) {
+  int rc = check_model(m, true);
+  if (rc) return rc;
+  if (B < 0 || (B > 0 && (!y || !h_out))) return fail(QCE_EARG, "bad y / h_out");
+  if (B == 0) return QCE_OK;
+  if (!qce_shape_supported(m->MP, m->NP)) return fail(QCE_ENOTIMPL, "shape not covered");
+  if (mode != QCE_MODE_ALL && m->K > 256) return fail(QCE_ENOTIMPL, "selective modes support K <= 256");
+  DeviceGuard g(m->device);
+  hipStream_t st = pick_stream(m, stream);
+  const double2* dy = nullptr;
+  if ((rc = stage_input(m, y, B, io, st, &dy))) return rc;
+  double2* dh = reinterpret_cast<double2*>(h_out);
+  if (io == QCE_IO_HOST) {
+    HIPCHK(m->h_scr.ensure((size_t)B * m->N));
+    dh = m->h_scr.p;
+  }
+  QceEstArgs a = est_args(m, dy, B);
+  if (mode == QCE_MODE_ALL) {
+    HIPCHK(qce_launch_est_all(a, dh, st));
+  } else {
+    int kmode, n = 0;
+    double p = 0.0;
+    if (mode == QCE_MODE_TOPN) {
+      if (mode_param < 1.0 || mode_param != floor(mode_param)) return fail(QCE_EARG, "top-n needs an integer n >= 1");
+      n = mode_param > 1e9 ? 1000000000 : (int)mode_param;
+      kmode = (n == 1) ? 3 : 1;
+    } else if (mode == QCE_MODE_CUMP) {
+      kmode = 2;
+      p = mode_param;
+    } else {
+      return fail(QCE_EARG, "unknown mode");
+    }
+    HIPCHK(m->lp_scr.ensure((size_t)B * m->K));
+    HIPCHK(m->w_scr.ensure((size_t)B * m->K));
+    HIPCHK(qce_launch_lp(a, m->lp_scr.p, st));
+    HIPCHK(qce_launch_select(B, m->K, m->lp_scr.p, kmode, n, p, nullptr, nullptr, m->w_scr.p, st));
+    HIPCHK(qce_launch_est_weighted(a, m->w_scr.p, dh, st));
+  }
+  if (io == QCE_IO_HOST) {
+    HIPCHK(hipMemcpyAsync(h_out, dh, sizeof(double2) * (size_t)B * m->N, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return QCE_OK;
+}
+
+int qce_log_prob(qce_model* m, const double* X, int64_t B, double* lp_out, double* proba_out, int64_t* labels_out,
+                 int io, void* stream) {
+  int rc = check_model(m, true);
+  if (rc) return rc;
+  if (B < 0 || (B > 0 && !X)) return fail(QCE_EARG, "bad X");
+  if (B == 0) return QCE_OK;
+  if (m->K > 256 && (proba_out || labels_out)) return fail(QCE_ENOTIMPL, "proba/labels support K <= 256");
+  DeviceGuard g(m->device);
+  hipStream_t st = pick_stream(m, stream);
+  const double2* dx = nullptr;
+  if ((rc = stage_input(m, X, B, io, st, &dx))) return rc;
+  QceEstArgs a = est_args(m, dx, B);
+  const size_t BK = (size_t)B * m->K;
+  double* dlp = lp_out;
+  double* dpr = proba_out;
+  long long* dlab = reinterpret_cast<long long*>(labels_out);
+  if (io == QCE_IO_HOST || !lp_out) {
+    HIPCHK(m->lp_scr.ensure(BK));
+    dlp = m->lp_scr.p;
+  }
+  if (io == QCE_IO_HOST && proba_out) {
+    HIPCHK(m->proba_scr.ensure(BK));
+    dpr = m->proba_scr.p;
+  }
+  if (io == QCE_IO_HOST && labels_out) {
+    HIPCHK(m->lab_scr.ensure((size_t)B));
+    dlab = m->lab_scr.p;
+  }
+  HIPCHK(qce_launch_lp(a, dlp, st));
+  if (proba_out || labels_out) HIPCHK(qce_launch_select(B, m->K, dlp, 0, 0, 0.0, dpr, dlab, nullptr, st));
+  if (io == QCE_IO_HOST) {
+    if (lp_out) HIPCHK(hipMemcpyAsync(lp_out, dlp, sizeof(double) * BK, hipMemcpyDeviceToHost, st));
+    if (proba_out) HIPCHK(hipMemcpyAsync(proba_out, dpr, sizeof(double) * BK, hipMemcpyDeviceToHost, st));
+    if (labels_out) HIPCHK(hipMemcpyAsync(labels_out, dlab, sizeof(int64_t) * B, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return QCE_OK;
+}
+
+int qce_estimate_partial(qce_model* m, const double* y, int64_t B, double* m_out, double* s_out, float* acc_out,
+                         int io, void* stream) {
+  int rc = check_model(m, true);
+  if (rc) return rc;
+  if (B < 0 || (B > 0 && (!y || !m_out || !s_out || !acc_out))) return fail(QCE_EARG, "bad arguments");
+  if (B == 0) return QCE_OK;
+  DeviceGuard g(m->device);
+  hipStream_t st = pick_stream(m, stream);
+  const double2* dy = nullptr;
+  if ((rc = stage_input(m, y, B, io, st, &dy))) return rc;
+  double *dm = m_out, *ds = s_out;
+  float* da = acc_out;
+  if (io == QCE_IO_HOST) {
+    HIPCHK(m->m_scr.ensure((size_t)B));
+    HIPCHK(m->s_scr.ensure((size_t)B));
+    HIPCHK(m->acc_scr.ensure((size_t)B * 2 * m->N));
+    dm = m->m_scr.p;
+    ds = m->s_scr.p;
+    da = m->acc_scr.p;
+  }
+  QceEstArgs a = est_args(m, dy, B);
+  HIPCHK(qce_launch_est_partial(a, dm, ds, da, st));
+  if (io == QCE_IO_HOST) {
+    HIPCHK(hipMemcpyAsync(m_out, dm, sizeof(double) * B, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(s_out, ds, sizeof(double) * B, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(acc_out, da, sizeof(float) * (size_t)B * 2 * m->N, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return QCE_OK;
+}
+
+int qce_get_tables(qce_model* m, double* means_y, double* Cy, double* Cr, double* P, double* A_eff, double* W,
+                   double* b, double* cconst) {
+  int rc = check_model(m, true);
+  if (rc) return rc;
+  DeviceGuard g(m->device);
+  hipStream_t st = m->stream;
+  const int K = m->K, M = m->M, N = m->N;
+  HIPCHK(hipStreamSynchronize(st));
+  auto cp = [&](double* dst, const void* src, size_t bytes) -> hipError_t {
+    if (!dst) return hipSuccess;
+    return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+  };
+  HIPCHK(cp(means_y, m->means_y.p, sizeof(double2) * (size_t)K * M));
+  HIPCHK(cp(Cy, m->Cy.p, sizeof(double2) * (size_t)K * M * M));
+  HIPCHK(cp(Cr, m->Cr.p, sizeof(double2) * (size_t)K * M * M));
+  HIPCHK(cp(A_eff, m->Aeff.p, sizeof(double2) * (size_t)K * M * N));
+  HIPCHK(cp(W, m->W.p, sizeof(double2) * (size_t)K * N * M));
+  HIPCHK(cp(b, m->bvec.p, sizeof(double2) * (size_t)K * N));
+  HIPCHK(cp(cconst, m->cconst.p, sizeof(double) * (size_t)K));
+  if (P) {
+    std::vector<double> li((size_t)2 * K * M * M);
+    HIPCHK(hipMemcpy(li.data(), m->Linv.p, sizeof(double2) * (size_t)K * M * M, hipMemcpyDeviceToHost));
+    for (int k = 0; k < K; ++k)
+      for (int i = 0; i < M; ++i)
+        for (int j = 0; j < M; ++j) {
+          const size_t src = ((size_t)k * M * M + (size_t)j * M + i) * 2;  // P[i][j] = conj(Linv[j][i])
+          const size_t dst = ((size_t)k * M * M + (size_t)i * M + j) * 2;
+          P[dst] = li[src];
+          P[dst + 1] = (j >= i) ? -li[src + 1] : 0.0;
+          if (j < i) P[dst] = 0.0;
+        }
+  }
+  return QCE_OK;
+}
+
+int qce_model_info(qce_model* m, int* K, int* N, int* M, int* device) {
+  if (!m) return fail(QCE_EARG, "null model");
+  if (K) *K = m->K;
+  if (N) *N = m->N;
+  if (M) *M = m->prepared ? m->M : 0;
+  if (device) *device = m->device;
+  return QCE_OK;
+}
+
+int qce_synchronize(qce_model* m) {
+  if (!m) return fail(QCE_EARG, "null model");
+  DeviceGuard g(m->device);
+  HIPCHK(hipStreamSynchronize(m->stream));
+  return QCE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,463 @@
+// Estimate-side kernels of the Bussgang-GMM estimator (gfx950 / CDNA4).
+//
+// Restated hot path (gmm_cplx_bussgang.py):
+//   lp[b,k] = c_k - || Linv_k (y_b - mu_y,k) ||^2                (:388-435, :369-386)
+//   gamma   = softmax_k lp                                        (:632-656, :351-367)
+//   'all'   : h_b = sum_k gamma_bk (W_k y_b + b_k)                (:220-228, :331-332)
+//   1 / n / p: selection over gamma, renormalised                 (:197-219, :229-242)
+//
+// k_est_all_f32 is a flash-style single pass over the K components for a tile of
+// 128 samples (4 waves x 32 samples): per component the whitened residual
+// u = E(Linv_k) [y;1] runs on v_mfma_f32_32x32x2_f32 (lower-triangular tiles skipped),
+// its squared norm gives lp in FP64, an online softmax (running max m, sum s) rescales the
+// accumulator, and Z = E(W_k) [y;1] on the same MFMA is folded in with weight e^{lp-m}.
+// The samples sit on the MFMA column (lane) axis, so every per-sample scalar (quad form,
+// m, s, weight) is a per-lane register and the Y^T fragments stay resident in VGPRs for
+// the whole K loop; component tables stream from L2 in fragment order (16 B per lane).
+#include "qce_common.h"
+#include "qce_kernels.h"
+
+#define QCE_NEG_INF (-__builtin_inf())
+
+template <int MP, int NP, bool HAS_MEAN, bool PARTIAL>
+__global__ __launch_bounds__(256, 2) void k_est_all_f32(long long B, int M, int N, int K, const double2* __restrict__ y,
+                                                        const float* __restrict__ pack, long long comp_stride,
+                                                        const double* __restrict__ cconst, double2* __restrict__ h,
+                                                        double* __restrict__ part_m, double* __restrict__ part_s,
+                                                        float* __restrict__ part_acc) {
+  constexpr int R = 2 * MP, S = 2 * NP;
+  constexpr int NSL = R / 32, NSW = S / 32;
+  constexpr int GW = MP / 4;
+  constexpr int HM = HAS_MEAN ? 1 : 0;
+  constexpr int GL_TOTAL = 2 * NSL * (NSL + 1) + HM * NSL;  // sum_r (4r+4+HM)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = lane & 31, hh = lane >> 5;
+  const long long sample = (long long)blockIdx.x * 128 + wave * 32 + j;
+  const bool valid = sample < B;
+
+  float yv[MP + HM];
+#pragma unroll
+  for (int s = 0; s < MP; ++s) {
+    float v = 0.0f;
+    if (valid && s < M) {
+      const double* yp = reinterpret_cast<const double*>(y + sample * M + s);
+      v = (float)yp[hh];
+    }
+    yv[s] = v;
+  }
+  if (HAS_MEAN) yv[MP] = hh ? 0.0f : 1.0f;
+
+  f32x16 out[NSW];
+#pragma unroll
+  for (int r = 0; r < NSW; ++r)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) out[r][q] = 0.0f;
+  double m = QCE_NEG_INF, ssum = 0.0;
+
+  for (int k = 0; k < K; ++k) {
+    const f32x4* __restrict__ pk = reinterpret_cast<const f32x4*>(pack + (long long)k * comp_stride) + lane;
+    double quad = 0.0;
+    int goff = 0;
+#pragma unroll
+    for (int r = 0; r < NSL; ++r) {
+      f32x16 acc;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+#pragma unroll
+      for (int g = 0; g < 4 * r + 4; ++g) {
+        f32x4 a = pk[(goff + g) * 64];
+        acc = mfma32x32x2(a[0], yv[4 * g + 0], acc);
+        acc = mfma32x32x2(a[1], yv[4 * g + 1], acc);
+        acc = mfma32x32x2(a[2], yv[4 * g + 2], acc);
+        acc = mfma32x32x2(a[3], yv[4 * g + 3], acc);
+      }
+      if (HAS_MEAN) {
+        f32x4 a = pk[(goff + 4 * r + 4) * 64];
+        acc = mfma32x32x2(a[0], yv[MP], acc);
+      }
+      goff += 4 * r + 4 + HM;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) quad = fma((double)acc[q], (double)acc[q], quad);
+    }
+    quad += __shfl_xor(quad, 32);
+    const double lp = cconst[k] - quad;
+    const double mnew = fmax(m, lp);
+    const double alpha = (m == mnew) ? 1.0 : exp(m - mnew);
+    const double p = (lp == QCE_NEG_INF) ? 0.0 : exp(lp - mnew);
+    ssum = ssum * alpha + p;
+    m = mnew;
+    const float af = (float)alpha, pf = (float)p;
+#pragma unroll
+    for (int r = 0; r < NSW; ++r) {
+      f32x16 acc;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+      const int base = GL_TOTAL + r * (GW + HM);
+#pragma unroll
+      for (int g = 0; g < GW; ++g) {
+        f32x4 a = pk[(base + g) * 64];
+        acc = mfma32x32x2(a[0], yv[4 * g + 0], acc);
+        acc = mfma32x32x2(a[1], yv[4 * g + 1], acc);
+        acc = mfma32x32x2(a[2], yv[4 * g + 2], acc);
+        acc = mfma32x32x2(a[3], yv[4 * g + 3], acc);
+      }
+      if (HAS_MEAN) {
+        f32x4 a = pk[(base + GW) * 64];
+        acc = mfma32x32x2(a[0], yv[MP], acc);
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) out[r][q] = fmaf(out[r][q], af, pf * acc[q]);
+    }
+  }
+
+  if (!valid) return;
+  if (PARTIAL) {
+    if (hh == 0) {
+      part_m[sample] = m;
+      part_s[sample] = ssum;
+    }
+    float* pa = part_acc + sample * (2LL * N);
+#pragma unroll
+    for (int r = 0; r < NSW; ++r)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n0 = 16 * r + 4 * q + 2 * hh;
+        if (n0 < N) {
+          pa[2 * n0] = out[r][4 * q + 0];
+          pa[2 * n0 + 1] = out[r][4 * q + 1];
+        }
+        if (n0 + 1 < N) {
+          pa[2 * n0 + 2] = out[r][4 * q + 2];
+          pa[2 * n0 + 3] = out[r][4 * q + 3];
+        }
+      }
+    return;
+  }
+  const double inv = 1.0 / ssum;
+  double2* hp = h + sample * N;
+#pragma unroll
+  for (int r = 0; r < NSW; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n0 = 16 * r + 4 * q + 2 * hh;
+      if (n0 < N) hp[n0] = make_double2((double)out[r][4 * q + 0] * inv, (double)out[r][4 * q + 1] * inv);
+      if (n0 + 1 < N) hp[n0 + 1] = make_double2((double)out[r][4 * q + 2] * inv, (double)out[r][4 * q + 3] * inv);
+    }
+}
+
+// h = sum_k w[b][k] (W_k y + b_k): the LMMSE half only, for the selective modes.  A
+// component no sample of the wave selected is skipped wave-uniformly.
+template <int MP, int NP, bool HAS_MEAN>
+__global__ __launch_bounds__(256, 2) void k_est_weighted_f32(long long B, int M, int N, int K,
+                                                             const double2* __restrict__ y,
+                                                             const float* __restrict__ pack, long long comp_stride,
+                                                             const float* __restrict__ wts, double2* __restrict__ h) {
+  constexpr int R = 2 * MP, S = 2 * NP;
+  constexpr int NSL = R / 32, NSW = S / 32;
+  constexpr int GW = MP / 4;
+  constexpr int HM = HAS_MEAN ? 1 : 0;
+  constexpr int GL_TOTAL = 2 * NSL * (NSL + 1) + HM * NSL;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = lane & 31, hh = lane >> 5;
+  const long long sample = (long long)blockIdx.x * 128 + wave * 32 + j;
+  const bool valid = sample < B;
+  float yv[MP + HM];
+#pragma unroll
+  for (int s = 0; s < MP; ++s) {
+    float v = 0.0f;
+    if (valid && s < M) {
+      const double* yp = reinterpret_cast<const double*>(y + sample * M + s);
+      v = (float)yp[hh];
+    }
+    yv[s] = v;
+  }
+  if (HAS_MEAN) yv[MP] = hh ? 0.0f : 1.0f;
+  f32x16 out[NSW];
+#pragma unroll
+  for (int r = 0; r < NSW; ++r)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) out[r][q] = 0.0f;
+  for (int k = 0; k < K; ++k) {
+    const float w = valid ? wts[sample * K + k] : 0.0f;
+    if (__ballot(w != 0.0f) == 0ull) continue;
+    const f32x4* __restrict__ pk = reinterpret_cast<const f32x4*>(pack + (long long)k * comp_stride) + lane;
+#pragma unroll
+    for (int r = 0; r < NSW; ++r) {
+      f32x16 acc;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+      const int base = GL_TOTAL + r * (GW + HM);
+#pragma unroll
+      for (int g = 0; g < GW; ++g) {
+        f32x4 a = pk[(base + g) * 64];
+        acc = mfma32x32x2(a[0], yv[4 * g + 0], acc);
+        acc = mfma32x32x2(a[1], yv[4 * g + 1], acc);
+        acc = mfma32x32x2(a[2], yv[4 * g + 2], acc);
+        acc = mfma32x32x2(a[3], yv[4 * g + 3], acc);
+      }
+      if (HAS_MEAN) {
+        f32x4 a = pk[(base + GW) * 64];
+        acc = mfma32x32x2(a[0], yv[MP], acc);
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) out[r][q] = fmaf(w, acc[q], out[r][q]);
+    }
+  }
+  if (!valid) return;
+  double2* hp = h + sample * N;
+#pragma unroll
+  for (int r = 0; r < NSW; ++r)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n0 = 16 * r + 4 * q + 2 * hh;
+      if (n0 < N) hp[n0] = make_double2((double)out[r][4 * q + 0], (double)out[r][4 * q + 1]);
+      if (n0 + 1 < N) hp[n0 + 1] = make_double2((double)out[r][4 * q + 2], (double)out[r][4 * q + 3]);
+    }
+}
+
+// lp[b][k] in FP64 on v_mfma_f64_16x16x4_f64 (exact argmax / ranking for the selective modes
+// and for predict_proba_cplx / _predict_cplx).  4 waves x 16 samples per workgroup.
+template <int MP, bool HAS_MEAN>
+__global__ __launch_bounds__(256, 2) void k_lp_f64(long long B, int M, int K, const double2* __restrict__ y,
+                                                   const double* __restrict__ pack, long long comp_stride,
+                                                   const double* __restrict__ cconst, double* __restrict__ lp) {
+  constexpr int R = 2 * MP;
+  constexpr int NSL = R / 16;
+  constexpr int NS = MP / 2;  // k-steps of 4 real columns
+  constexpr int HM = HAS_MEAN ? 1 : 0;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const long long sample = (long long)blockIdx.x * 64 + wave * 16 + (lane & 15);
+  const bool valid = sample < B;
+  double yd[NS + HM];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int c = 2 * s + (lane >> 5), part = (lane >> 4) & 1;
+    double v = 0.0;
+    if (valid && c < M) v = reinterpret_cast<const double*>(y + sample * M + c)[part];
+    yd[s] = v;
+  }
+  if (HAS_MEAN) yd[NS] = (lane >> 4) == 0 ? 1.0 : 0.0;
+  for (int k = 0; k < K; ++k) {
+    const double* __restrict__ pk = pack + (long long)k * comp_stride + lane;
+    double quad = 0.0;
+    int soff = 0;
+#pragma unroll
+    for (int r = 0; r < NSL; ++r) {
+      f64x4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int s = 0; s < 4 * r + 4; ++s) acc = mfma16x16x4d(pk[(soff + s) * 64], yd[s], acc);
+      if (HAS_MEAN) acc = mfma16x16x4d(pk[(soff + 4 * r + 4) * 64], yd[NS], acc);
+      soff += 4 * r + 4 + HM;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) quad = fma(acc[q], acc[q], quad);
+    }
+    quad += __shfl_xor(quad, 16);
+    quad += __shfl_xor(quad, 32);
+    if (valid && (lane >> 4) == 0) lp[sample * K + k] = cconst[k] - quad;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// per-sample selection, one wave per sample (K <= 256: 4 values per lane)
+// ---------------------------------------------------------------------------
+QCE_DEV double wave_max(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  return v;
+}
+QCE_DEV double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+// argmax with (value, index) ordering: larger value wins; on ties prefer_low selects the lower index
+QCE_DEV void wave_argmax(double& v, int& idx, bool prefer_low) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    double ov = __shfl_xor(v, o);
+    int oi = __shfl_xor(idx, o);
+    bool take = (ov > v) || (ov == v && (prefer_low ? (oi < idx) : (oi > idx)));
+    if (take) {
+      v = ov;
+      idx = oi;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_select(long long B, int K, const double* __restrict__ lp, int mode, int nsel,
+                                                double psel, double* __restrict__ proba, long long* __restrict__ labels,
+                                                float* __restrict__ wts) {
+  const int lane = threadIdx.x & 63;
+  const long long b = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const double* row = lp + b * K;
+  double v[4];
+  int taken = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = lane + 64 * i;
+    v[i] = k < K ? row[k] : QCE_NEG_INF;
+  }
+  // labels: first index of max lp (numpy argmax)
+  double bv = QCE_NEG_INF;
+  int bi = 1 << 30;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = lane + 64 * i;
+    if (k < K && (v[i] > bv || (v[i] == bv && k < bi) || bi == (1 << 30))) {
+      bv = v[i];
+      bi = k;
+    }
+  }
+  wave_argmax(bv, bi, true);
+  if (labels && lane == 0) labels[b] = bi;
+  // logsumexp (scipy.special.logsumexp) -> proba = exp(lp - lse)
+  const double mx = wave_max(fmax(fmax(v[0], v[1]), fmax(v[2], v[3])));
+  double t = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (lane + 64 * i < K) t += exp(v[i] - mx);
+  const double lse = log(wave_sum(t)) + mx;
+  double pr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) pr[i] = (lane + 64 * i < K) ? exp(v[i] - lse) : -1.0;
+  if (proba) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (lane + 64 * i < K) proba[b * K + lane + 64 * i] = pr[i];
+  }
+  if (!wts) return;
+  float w[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (mode == 3 || (mode == 1 && nsel == 1)) {  // argmax path (:200-207): h = h_label, weight exactly 1
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (lane + 64 * i == bi) w[i] = 1.0f;
+  } else if (mode == 1 || mode == 2) {
+    // descending-proba selection (:213 / :235-236); ties broken towards the higher index,
+    // matching a reversed stable ascending sort
+    double cum = 0.0;
+    double chosen[4] = {0.0, 0.0, 0.0, 0.0};
+    const int limit = (mode == 1) ? (nsel < K ? nsel : K) : K;
+    for (int it = 0; it < limit; ++it) {
+      double cv = -2.0;
+      int ci = -1;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int k = lane + 64 * i;
+        if (k < K && !((taken >> i) & 1) && (pr[i] > cv || (pr[i] == cv && k > ci))) {
+          cv = pr[i];
+          ci = k;
+        }
+      }
+      wave_argmax(cv, ci, false);
+      if (ci < 0) break;
+      if ((ci & 63) == lane) {
+        taken |= 1 << (ci >> 6);
+        chosen[ci >> 6] = cv;
+      }
+      cum += cv;
+      if (mode == 2 && cum >= psel) break;
+    }
+    // normalise by the sum of the selected probabilities (:219 / :242)
+    double tot = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if ((taken >> i) & 1) tot += chosen[i];
+    tot = wave_sum(tot);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if ((taken >> i) & 1) w[i] = (float)(chosen[i] / tot);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (lane + 64 * i < K) wts[b * K + lane + 64 * i] = w[i];
+}
+
+// ---------------------------------------------------------------------------
+// dispatch
+// ---------------------------------------------------------------------------
+bool qce_shape_supported(int MP, int NP) {
+  auto ok = [](int v) { return v == 16 || v == 32 || v == 64; };
+  return ok(MP) && ok(NP);
+}
+
+template <int MP, int NP, bool HM>
+static hipError_t launch_all_t(const QceEstArgs& a, double2* h, double* pm, double* ps, float* pa, bool partial,
+                               hipStream_t st) {
+  dim3 grid((unsigned)((a.B + 127) / 128));
+  if (partial)
+    hipLaunchKernelGGL((k_est_all_f32<MP, NP, HM, true>), grid, dim3(256), 0, st, a.B, a.M, a.N, a.K, a.y, a.pack32,
+                       a.stride32, a.cconst, h, pm, ps, pa);
+  else
+    hipLaunchKernelGGL((k_est_all_f32<MP, NP, HM, false>), grid, dim3(256), 0, st, a.B, a.M, a.N, a.K, a.y, a.pack32,
+                       a.stride32, a.cconst, h, pm, ps, pa);
+  return hipGetLastError();
+}
+
+template <int MP, int NP, bool HM>
+static hipError_t launch_w_t(const QceEstArgs& a, const float* w, double2* h, hipStream_t st) {
+  dim3 grid((unsigned)((a.B + 127) / 128));
+  hipLaunchKernelGGL((k_est_weighted_f32<MP, NP, HM>), grid, dim3(256), 0, st, a.B, a.M, a.N, a.K, a.y, a.pack32,
+                     a.stride32, w, h);
+  return hipGetLastError();
+}
+
+template <int MP, bool HM>
+static hipError_t launch_lp_t(const QceEstArgs& a, double* lp, hipStream_t st) {
+  dim3 grid((unsigned)((a.B + 63) / 64));
+  hipLaunchKernelGGL((k_lp_f64<MP, HM>), grid, dim3(256), 0, st, a.B, a.M, a.K, a.y, a.pack64, a.stride64, a.cconst,
+                     lp);
+  return hipGetLastError();
+}
+
+#define QCE_FOR_SHAPES(X) \
+  X(16, 16) X(16, 32) X(16, 64) X(32, 16) X(32, 32) X(32, 64) X(64, 16) X(64, 32) X(64, 64)
+
+hipError_t qce_launch_est_all(const QceEstArgs& a, double2* h, hipStream_t st) {
+  const bool hm = a.has_mean != 0;
+#define QCE_CASE(X, Y)                                                                      \
+  if (a.MP == X && a.NP == Y)                                                               \
+    return hm ? launch_all_t<X, Y, true>(a, h, nullptr, nullptr, nullptr, false, st)        \
+              : launch_all_t<X, Y, false>(a, h, nullptr, nullptr, nullptr, false, st);
+  QCE_FOR_SHAPES(QCE_CASE)
+#undef QCE_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t qce_launch_est_partial(const QceEstArgs& a, double* m, double* s, float* acc, hipStream_t st) {
+  const bool hm = a.has_mean != 0;
+#define QCE_CASE(X, Y)                                                                      \
+  if (a.MP == X && a.NP == Y)                                                               \
+    return hm ? launch_all_t<X, Y, true>(a, nullptr, m, s, acc, true, st)                   \
+              : launch_all_t<X, Y, false>(a, nullptr, m, s, acc, true, st);
+  QCE_FOR_SHAPES(QCE_CASE)
+#undef QCE_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t qce_launch_est_weighted(const QceEstArgs& a, const float* w, double2* h, hipStream_t st) {
+  const bool hm = a.has_mean != 0;
+#define QCE_CASE(X, Y) \
+  if (a.MP == X && a.NP == Y) return hm ? launch_w_t<X, Y, true>(a, w, h, st) : launch_w_t<X, Y, false>(a, w, h, st);
+  QCE_FOR_SHAPES(QCE_CASE)
+#undef QCE_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t qce_launch_lp(const QceEstArgs& a, double* lp, hipStream_t st) {
+  const bool hm = a.has_mean != 0;
+  switch (a.MP) {
+    case 16: return hm ? launch_lp_t<16, true>(a, lp, st) : launch_lp_t<16, false>(a, lp, st);
+    case 32: return hm ? launch_lp_t<32, true>(a, lp, st) : launch_lp_t<32, false>(a, lp, st);
+    case 64: return hm ? launch_lp_t<64, true>(a, lp, st) : launch_lp_t<64, false>(a, lp, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t qce_launch_select(long long B, int K, const double* lp, int mode, int n, double p, double* proba,
+                             long long* labels, float* wts, hipStream_t st) {
+  if (K > 256) return hipErrorInvalidValue;
+  dim3 grid((unsigned)((B + 3) / 4));
+  hipLaunchKernelGGL(k_select, grid, dim3(256), 0, st, B, K, lp, mode, n, p, proba, labels, wts);
+  return hipGetLastError();
+}

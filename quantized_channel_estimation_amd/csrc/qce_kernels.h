@@ -1,0 +1,52 @@
+// Internal launch interface between the C-ABI layer (qce_capi.hip) and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+struct QcePrepareArgs {
+  int K, N, M, MP, NP, has_mean, identityA;
+  int kind;        // 0: 1 bit, 1: multi-bit, 2: n_bits = inf
+  int n_bits;      // multi-bit only
+  int quant_kind;  // 0 uniform, 1 lloyd, 2 other (zero gain)
+  double sigma2, delta;
+  const double* thr;  // device, 2^b - 1 entries
+  const double* lab;  // device, 2^b entries
+  const double2* A;   // M x N
+  const double2* covs;
+  const double2* means;
+  const double* logw;
+  double2 *Cy, *Cr, *Lw, *Linv, *Aeff, *work, *V, *W, *means_y, *q0, *bvec;
+  double *gain, *cconst;
+  int* status;
+  float* pack32;
+  long long stride32;
+  double* pack64;
+  long long stride64;
+};
+
+long long qce_pack_f32_stride(int MP, int NP, int has_mean);
+long long qce_pack_f64_stride(int MP, int has_mean);
+hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st);
+
+struct QceEstArgs {
+  long long B;
+  int M, N, K, MP, NP, has_mean;
+  const double2* y;  // B x M (row stride M)
+  const float* pack32;
+  long long stride32;
+  const double* pack64;
+  long long stride64;
+  const double* cconst;
+};
+
+// 'all' mode, fused responsibilities + LMMSE combination; h = B x N complex128
+hipError_t qce_launch_est_all(const QceEstArgs& a, double2* h, hipStream_t st);
+// K-shard partial: m, s (B doubles), acc (B x 2N floats, un-normalised, interleaved re/im)
+hipError_t qce_launch_est_partial(const QceEstArgs& a, double* m, double* s, float* acc, hipStream_t st);
+// weighted log-probabilities lp[b][k] (FP64), row stride K
+hipError_t qce_launch_lp(const QceEstArgs& a, double* lp, hipStream_t st);
+// selection: mode 0 = proba only, 1 = top-n, 2 = cumulative-p, 3 = argmax(lp)
+hipError_t qce_launch_select(long long B, int K, const double* lp, int mode, int n, double p, double* proba,
+                             long long* labels, float* wts, hipStream_t st);
+// h = sum_k wts[b][k] (W_k y_b + b_k)
+hipError_t qce_launch_est_weighted(const QceEstArgs& a, const float* wts, double2* h, hipStream_t st);
+bool qce_shape_supported(int MP, int NP);

@@ -1,0 +1,460 @@
+// Per-SNR precompute of the Bussgang-GMM estimator, FP64 on the device.
+//
+// Restates gmm_cplx_bussgang.py:246-328 (_prepare_for_prediction) and :15-82
+// (compute_precision_cholesky / _compute_log_det_cholesky) as batched kernels:
+//   Cy_k = A C_k A^H + s2 I                                   (:267-271)
+//   g_k  = Bussgang gain of diag(Cy_k)                         (:273-284, uniform_quantizer.py:60-72,
+//                                                               lloyd_max_quantizer.py:10-21)
+//   mu_y = g_k * (A mu_k)                                     (:256-264, :287-288)
+//   Cr_k = arcsine law | beta-mix | Cy                         (:290-307)
+//   L_k L_k^H = Cr_k,  Linv_k = L_k^{-1},  P_k = Linv_k^H       (:310, :15-52)
+//   c_k  = -M log(pi) + 2 sum log diag(P_k) + log w_k          (:411, :435, :383)
+//   W_k  = C_k Aeff_k^H Cr_k^{-1} = (C_k (Linv_k Aeff_k)^H) Linv_k (:321-326 with the Cholesky
+//          factor in place of pinv; Cr_k is Hermitian PD, see SURVEY.md Appendix A note)
+//   q0_k = Linv_k mu_y,k ; b_k = mu_k - W_k mu_y,k              (:331-332, algebraic form)
+// and packs the FP32 / FP64 fragment-ordered component tables the estimate
+// kernels stream (qce_estimate.hip).
+#include "qce_common.h"
+#include "qce_kernels.h"
+
+// ---------------------------------------------------------------------------
+// batched complex GEMM, row-major, C = alpha op(A) op(B) + beta C
+// op: 0 = N, 1 = T, 2 = C (conjugate transpose).  32x32 output tile / 256 threads.
+// ---------------------------------------------------------------------------
+template <int OPA, int OPB>
+__global__ __launch_bounds__(256) void k_zgemm(int m, int n, int k, double2 alpha, const double2* __restrict__ A, int lda,
+                                               long long sA, const double2* __restrict__ B, int ldb, long long sB,
+                                               double2 beta, double2* __restrict__ C, int ldc, long long sC) {
+  __shared__ double2 As[16][33];
+  __shared__ double2 Bs[16][33];
+  const int z = blockIdx.z;
+  A += z * sA;
+  B += z * sB;
+  C += z * sC;
+  const int row0 = blockIdx.y * 32, col0 = blockIdx.x * 32;
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  double2 acc[2][2];
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) acc[a][b] = make_double2(0.0, 0.0);
+  for (int k0 = 0; k0 < k; k0 += 16) {
+    for (int e = tid; e < 512; e += 256) {
+      int i, l;
+      double2 v = make_double2(0.0, 0.0);
+      if (OPA == 0) {
+        l = e & 15;
+        i = e >> 4;
+        if (row0 + i < m && k0 + l < k) v = A[(long long)(row0 + i) * lda + k0 + l];
+      } else {
+        i = e & 31;
+        l = e >> 5;
+        if (row0 + i < m && k0 + l < k) v = A[(long long)(k0 + l) * lda + row0 + i];
+        if (OPA == 2) v.y = -v.y;
+      }
+      As[l][i] = v;
+      int j;
+      v = make_double2(0.0, 0.0);
+      if (OPB == 0) {
+        j = e & 31;
+        l = e >> 5;
+        if (k0 + l < k && col0 + j < n) v = B[(long long)(k0 + l) * ldb + col0 + j];
+      } else {
+        l = e & 15;
+        j = e >> 4;
+        if (k0 + l < k && col0 + j < n) v = B[(long long)(col0 + j) * ldb + k0 + l];
+        if (OPB == 2) v.y = -v.y;
+      }
+      Bs[l][j] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int l = 0; l < 16; ++l) {
+      double2 a0 = As[l][ty * 2], a1 = As[l][ty * 2 + 1];
+      double2 b0 = Bs[l][tx * 2], b1 = Bs[l][tx * 2 + 1];
+      acc[0][0] = cfma(a0, b0, acc[0][0]);
+      acc[0][1] = cfma(a0, b1, acc[0][1]);
+      acc[1][0] = cfma(a1, b0, acc[1][0]);
+      acc[1][1] = cfma(a1, b1, acc[1][1]);
+    }
+    __syncthreads();
+  }
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b) {
+      int r = row0 + ty * 2 + a, c = col0 + tx * 2 + b;
+      if (r < m && c < n) {
+        double2* p = C + (long long)r * ldc + c;
+        double2 v = cmul(alpha, acc[a][b]);
+        if (beta.x != 0.0 || beta.y != 0.0) v = cadd(v, cmul(beta, *p));
+        *p = v;
+      }
+    }
+}
+
+static hipError_t zgemm(int opa, int opb, int m, int n, int k, double2 alpha, const double2* A, int lda, long long sA,
+                        const double2* B, int ldb, long long sB, double2 beta, double2* C, int ldc, long long sC,
+                        int batch, hipStream_t st) {
+  dim3 grid((n + 31) / 32, (m + 31) / 32, batch);
+#define ZG(OA, OB)                                                                                              \
+  if (opa == OA && opb == OB) {                                                                                 \
+    hipLaunchKernelGGL((k_zgemm<OA, OB>), grid, dim3(256), 0, st, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, \
+                       C, ldc, sC);                                                                             \
+    return hipGetLastError();                                                                                   \
+  }
+  ZG(0, 0) ZG(0, 2) ZG(2, 0) ZG(0, 1)
+#undef ZG
+  return hipErrorInvalidValue;
+}
+
+// Cy = C + s2 I  (A = I fast path; numerically identical to I C I^H + s2 I)
+__global__ void k_cy_identity(int N, long long total, const double2* __restrict__ C, double2* __restrict__ Cy, double s2) {
+  long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  int rc = (int)(idx % ((long long)N * N));
+  double2 v = C[idx];
+  if (rc / N == rc % N) v.x += s2;
+  Cy[idx] = v;
+}
+
+__global__ void k_diag_add(int M, int K, double2* __restrict__ Cy, double s2) {
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= K * M) return;
+  int k = idx / M, i = idx % M;
+  Cy[(long long)k * M * M + (long long)i * M + i].x += s2;
+}
+
+// ---------------------------------------------------------------------------
+// Bussgang gain, observation mean and Cr per component (one workgroup per k)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_gain_cr(int M, int N, const double2* __restrict__ Cy, double2* __restrict__ Cr,
+                                                 double* __restrict__ gain, const double2* __restrict__ A,
+                                                 const double2* __restrict__ means, double2* __restrict__ means_y,
+                                                 double2* __restrict__ Aeff, int kind, int n_bits, int quant_kind,
+                                                 double delta, const double* __restrict__ thr,
+                                                 const double* __restrict__ lab) {
+  const int k = blockIdx.x, tid = threadIdx.x;
+  const double2* cy = Cy + (long long)k * M * M;
+  double2* cr = Cr + (long long)k * M * M;
+  double* g = gain + (long long)k * M;
+  __shared__ double s_beta;
+  const double PI = 3.14159265358979323846;
+  for (int i = tid; i < M; i += 256) {
+    double d = cy[(long long)i * M + i].x;
+    double gi;
+    if (kind == 0) {  // 1 bit (:277)
+      gi = sqrt(2.0 / PI) * (1.0 / sqrt(d));
+    } else if (kind == 2) {  // n_bits = inf (:278-279)
+      gi = 1.0;
+    } else if (quant_kind == 0) {  // uniform, uniform_quantizer.py:66-71
+      const int L = 1 << n_bits;
+      double dinv = 1.0 / d, acc = 0.0;
+      for (int q = 1; q < L; ++q) {
+        double o = (double)q - (double)L / 2.0;
+        acc += exp(-delta * delta * (o * o) * dinv);
+      }
+      gi = acc * (delta / sqrt(PI) / sqrt(d));
+    } else if (quant_kind == 1) {  // Lloyd-Max, lloyd_max_quantizer.py:11-20; thr has L-1 entries
+      const int L = 1 << n_bits;
+      double dinv = 1.0 / d;
+      double acc = -lab[0] * exp(-thr[0] * thr[0] * dinv);
+      acc += lab[L - 1] * exp(-thr[L - 2] * thr[L - 2] * dinv);
+      for (int q = 1; q < L - 1; ++q)
+        acc += lab[q] * (exp(-thr[q - 1] * thr[q - 1] * dinv) - exp(-thr[q] * thr[q] * dinv));
+      gi = acc / (sqrt(PI) * sqrt(d));
+    } else {  // unknown multi-bit quantiser type: the reference leaves A_buss = 0 (:281-284)
+      gi = 0.0;
+    }
+    g[i] = gi;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double s = 0.0;
+    for (int i = 0; i < M; ++i) s += g[i];
+    double beta = s / M;
+    s_beta = beta < 0.0 ? 0.0 : (beta > 1.0 ? 1.0 : beta);
+  }
+  __syncthreads();
+  const double beta2 = s_beta * s_beta;
+  const double two_over_pi = 2.0 / PI;
+  for (long long e = tid; e < (long long)M * M; e += 256) {
+    int i = (int)(e / M), j = (int)(e % M);
+    double2 v = cy[e];
+    double2 o;
+    if (kind == 0) {  // arcsine law (:292-301)
+      double pi_ = 1.0 / sqrt(cy[(long long)i * M + i].x);
+      double pj_ = 1.0 / sqrt(cy[(long long)j * M + j].x);
+      double re = (pi_ * v.x) * pj_, im = (pi_ * v.y) * pj_;
+      re = re > 1.0 ? 1.0 : (re < -1.0 ? -1.0 : re);
+      im = im > 1.0 ? 1.0 : (im < -1.0 ? -1.0 : im);
+      o = make_double2(two_over_pi * asin(re), two_over_pi * asin(im));
+    } else if (kind == 2) {
+      o = v;
+    } else {  // beta-mix (:305-307)
+      o = make_double2(beta2 * v.x, beta2 * v.y);
+      if (i == j) o = make_double2(o.x + (1.0 - beta2) * v.x, o.y + (1.0 - beta2) * v.y);
+    }
+    cr[e] = o;
+  }
+  // mu_y = g * (A mu_k);  Aeff = diag(g) A
+  const double2* mu = means + (long long)k * N;
+  for (int i = tid; i < M; i += 256) {
+    double2 am = make_double2(0.0, 0.0);
+    for (int n = 0; n < N; ++n) am = cfma(A[(long long)i * N + n], mu[n], am);
+    means_y[(long long)k * M + i] = cscale(am, g[i]);
+  }
+  for (long long e = tid; e < (long long)M * N; e += 256) {
+    int i = (int)(e / N);
+    Aeff[(long long)k * M * N + e] = cscale(A[e], g[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Cholesky (lower, right-looking) + lower-triangular inverse, one workgroup per k.
+// Lw holds a copy of Cr_k on entry and L_k on exit (lower part).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_chol_inv(int M, double2* __restrict__ Lw, double2* __restrict__ Linv,
+                                                  const double* __restrict__ logw, double* __restrict__ cconst,
+                                                  int* __restrict__ status) {
+  const int k = blockIdx.x, tid = threadIdx.x;
+  double2* a = Lw + (long long)k * M * M;
+  double2* x = Linv + (long long)k * M * M;
+  __shared__ double s_piv;
+  __shared__ int s_bad;
+  if (tid == 0) s_bad = 0;
+  __syncthreads();
+  for (int j = 0; j < M; ++j) {
+    if (tid == 0) {
+      double ajj = a[(long long)j * M + j].x;
+      if (!(ajj > 0.0)) s_bad = 1;
+      ajj = sqrt(ajj);
+      a[(long long)j * M + j] = make_double2(ajj, 0.0);
+      s_piv = ajj;
+    }
+    __syncthreads();
+    if (s_bad) break;
+    const double piv = s_piv;
+    for (int i = j + 1 + tid; i < M; i += 256) {
+      double2 v = a[(long long)i * M + j];
+      a[(long long)i * M + j] = make_double2(v.x / piv, v.y / piv);
+    }
+    __syncthreads();
+    const int n = M - j - 1;
+    for (int t = tid; t < n * n; t += 256) {
+      int r = j + 1 + t / n, c = j + 1 + t % n;
+      if (c > r) continue;
+      double2 lr = a[(long long)r * M + j], lc = a[(long long)c * M + j];
+      a[(long long)r * M + c] = csub(a[(long long)r * M + c], cmulc(lr, lc));
+    }
+    __syncthreads();
+  }
+  if (s_bad) {
+    if (tid == 0) status[k] = 1;
+    return;
+  }
+  for (long long e = tid; e < (long long)M * M; e += 256) {
+    int r = (int)(e / M), c = (int)(e % M);
+    x[e] = make_double2(r == c ? 1.0 : 0.0, 0.0);
+  }
+  __syncthreads();
+  for (int kk = 0; kk < M; ++kk) {
+    const double d = a[(long long)kk * M + kk].x;
+    for (int c = tid; c <= kk; c += 256) {
+      double2 v = x[(long long)kk * M + c];
+      x[(long long)kk * M + c] = make_double2(v.x / d, v.y / d);
+    }
+    __syncthreads();
+    const int nr = M - kk - 1, nc = kk + 1;
+    for (int t = tid; t < nr * nc; t += 256) {
+      int i = kk + 1 + t / nc, c = t % nc;
+      x[(long long)i * M + c] = csub(x[(long long)i * M + c], cmul(a[(long long)i * M + kk], x[(long long)kk * M + c]));
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    double ld = 0.0;
+    for (int i = 0; i < M; ++i) ld += log(x[(long long)i * M + i].x);
+    cconst[k] = -(M * log(3.14159265358979323846)) + 2.0 * ld + logw[k];
+    status[k] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Packing of the FP32 fused-kernel tables (32x32x2 MFMA A-operand order).
+// Real embedding with interleaved (re, im): E[2i][2j]=Re, E[2i][2j+1]=-Im, E[2i+1][2j]=Im, E[2i+1][2j+1]=Re.
+// Per component: GL slices r=0..R/32-1 with 4r+4 groups (+1 mean group), then GW slices
+// r=0..S/32-1 with MP/4 groups (+1 mean group).  A group = 64 lanes x 4 floats:
+//   lane l, elem t -> E[32r + (l&31)][8g + 2t + (l>>5)]
+// The mean group holds column R (= -q0 for GL, b for GW) in t=0 of lanes 0..31.
+// ---------------------------------------------------------------------------
+QCE_DEV float embed(const double2* Mx, int ld, int rows, int cols, int r, int c) {
+  int i = r >> 1, j = c >> 1;
+  if (i >= rows || j >= cols) return 0.0f;
+  double2 v = Mx[(long long)i * ld + j];
+  int rr = r & 1, cc = c & 1;
+  double o = (rr == cc) ? v.x : (rr == 0 ? -v.y : v.y);
+  return (float)o;
+}
+
+__global__ __launch_bounds__(256) void k_pack_f32(int M, int N, int MP, int NP, int has_mean, long long comp_stride,
+                                                  const double2* __restrict__ Linv, const double2* __restrict__ W,
+                                                  const double2* __restrict__ q0, const double2* __restrict__ bvec,
+                                                  float* __restrict__ pack) {
+  const int k = blockIdx.y;
+  const int R = 2 * MP, S = 2 * NP;
+  const int nsl_l = R / 32, nsl_w = S / 32;
+  const int tid = threadIdx.x, lane = tid >> 2, t = tid & 3;
+  const double2* L = Linv + (long long)k * M * M;
+  const double2* Wk = W + (long long)k * N * M;
+  float* out = pack + (long long)k * comp_stride;
+  int sl = blockIdx.x;
+  long long off = 0;
+  if (sl < nsl_l) {
+    int r = sl;
+    for (int q = 0; q < r; ++q) off += (long long)(4 * q + 4 + has_mean) * 256;
+    const int G = 4 * r + 4;
+    const int row = 32 * r + (lane & 31);
+    for (int g = 0; g < G + has_mean; ++g) {
+      float v;
+      if (g < G) {
+        int col = 8 * g + 2 * t + (lane >> 5);
+        v = embed(L, M, M, M, row, col);
+      } else {
+        v = 0.0f;
+        if (t == 0 && lane < 32 && (row >> 1) < M) {
+          double2 qv = q0[(long long)k * M + (row >> 1)];
+          v = (float)(-((row & 1) ? qv.y : qv.x));
+        }
+      }
+      out[off + (long long)g * 256 + tid] = v;
+    }
+  } else {
+    int r = sl - nsl_l;
+    for (int q = 0; q < nsl_l; ++q) off += (long long)(4 * q + 4 + has_mean) * 256;
+    const int G = MP / 4;
+    off += (long long)r * (G + has_mean) * 256;
+    const int row = 32 * r + (lane & 31);
+    for (int g = 0; g < G + has_mean; ++g) {
+      float v;
+      if (g < G) {
+        int col = 8 * g + 2 * t + (lane >> 5);
+        v = embed(Wk, M, N, M, row, col);
+      } else {
+        v = 0.0f;
+        if (t == 0 && lane < 32 && (row >> 1) < N) {
+          double2 bv = bvec[(long long)k * N + (row >> 1)];
+          v = (float)((row & 1) ? bv.y : bv.x);
+        }
+      }
+      out[off + (long long)g * 256 + tid] = v;
+    }
+  }
+}
+
+// FP64 lp tables (16x16x4 f64 MFMA A-operand order): slice r = 16 real rows, k-step s covers
+// real columns 4s..4s+3; lane l -> E[16r + (l&15)][4s + (l>>4)].  Slice r holds k-steps
+// 0..4r+3 (lower-triangular skip) plus one mean k-step (column R = -q0) when has_mean.
+__global__ __launch_bounds__(64) void k_pack_f64(int M, int MP, int has_mean, long long comp_stride,
+                                                 const double2* __restrict__ Linv, const double2* __restrict__ q0,
+                                                 double* __restrict__ pack) {
+  const int k = blockIdx.y, r = blockIdx.x, lane = threadIdx.x;
+  const double2* L = Linv + (long long)k * M * M;
+  double* out = pack + (long long)k * comp_stride;
+  long long off = 0;
+  for (int q = 0; q < r; ++q) off += (long long)(4 * q + 4 + has_mean) * 64;
+  const int S = 4 * r + 4;
+  const int row = 16 * r + (lane & 15);
+  for (int s = 0; s < S + has_mean; ++s) {
+    double v = 0.0;
+    if (s < S) {
+      int col = 4 * s + (lane >> 4);
+      int i = row >> 1, j = col >> 1;
+      if (i < M && j < M) {
+        double2 e = L[(long long)i * M + j];
+        int rr = row & 1, cc = col & 1;
+        v = (rr == cc) ? e.x : (rr == 0 ? -e.y : e.y);
+      }
+    } else if ((lane >> 4) == 0 && (row >> 1) < M) {
+      double2 qv = q0[(long long)k * M + (row >> 1)];
+      v = -((row & 1) ? qv.y : qv.x);
+    }
+    out[off + (long long)s * 64 + lane] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launch helpers (called from qce_capi.cpp)
+// ---------------------------------------------------------------------------
+long long qce_pack_f32_stride(int MP, int NP, int has_mean) {
+  const int R = 2 * MP, S = 2 * NP;
+  long long n = 0;
+  for (int r = 0; r < R / 32; ++r) n += (long long)(4 * r + 4 + has_mean) * 256;
+  n += (long long)(S / 32) * (MP / 4 + has_mean) * 256;
+  return n;
+}
+
+long long qce_pack_f64_stride(int MP, int has_mean) {
+  const int R = 2 * MP;
+  long long n = 0;
+  for (int r = 0; r < R / 16; ++r) n += (long long)(4 * r + 4 + has_mean) * 64;
+  return n;
+}
+
+hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
+  const int K = p.K, N = p.N, M = p.M;
+  hipError_t e;
+  const double2 one = make_double2(1.0, 0.0), zero = make_double2(0.0, 0.0), mone = make_double2(-1.0, 0.0);
+  // Cy
+  if (p.identityA) {
+    long long total = (long long)K * N * N;
+    hipLaunchKernelGGL(k_cy_identity, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, N, total, p.covs, p.Cy,
+                       p.sigma2);
+  } else {
+    // T = A C_k (M x N), Cy = T A^H (M x M)
+    if ((e = zgemm(0, 0, M, N, N, one, p.A, N, 0, p.covs, N, (long long)N * N, zero, p.work, N, (long long)M * N, K,
+                   st)) != hipSuccess)
+      return e;
+    if ((e = zgemm(0, 2, M, M, N, one, p.work, N, (long long)M * N, p.A, N, 0, zero, p.Cy, M, (long long)M * M, K,
+                   st)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(k_diag_add, dim3((K * M + 255) / 256), dim3(256), 0, st, M, K, p.Cy, p.sigma2);
+  }
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_gain_cr, dim3(K), dim3(256), 0, st, M, N, p.Cy, p.Cr, p.gain, p.A, p.means, p.means_y, p.Aeff,
+                     p.kind, p.n_bits, p.quant_kind, p.delta, p.thr, p.lab);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = hipMemcpyAsync(p.Lw, p.Cr, sizeof(double2) * (size_t)K * M * M, hipMemcpyDeviceToDevice, st)) != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(k_chol_inv, dim3(K), dim3(256), 0, st, M, p.Lw, p.Linv, p.logw, p.cconst, p.status);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // X = Linv Aeff (M x N) -> work
+  if ((e = zgemm(0, 0, M, N, M, one, p.Linv, M, (long long)M * M, p.Aeff, N, (long long)M * N, zero, p.work, N,
+                 (long long)M * N, K, st)) != hipSuccess)
+    return e;
+  // V = C X^H (N x M)
+  if ((e = zgemm(0, 2, N, M, N, one, p.covs, N, (long long)N * N, p.work, N, (long long)M * N, zero, p.V, M,
+                 (long long)N * M, K, st)) != hipSuccess)
+    return e;
+  // W = V Linv (N x M)
+  if ((e = zgemm(0, 0, N, M, M, one, p.V, M, (long long)N * M, p.Linv, M, (long long)M * M, zero, p.W, M,
+                 (long long)N * M, K, st)) != hipSuccess)
+    return e;
+  // q0 = Linv mu_y (M x 1);  b = mu - V q0 (N x 1)
+  if ((e = zgemm(0, 0, M, 1, M, one, p.Linv, M, (long long)M * M, p.means_y, 1, M, zero, p.q0, 1, M, K, st)) !=
+      hipSuccess)
+    return e;
+  if ((e = hipMemcpyAsync(p.bvec, p.means, sizeof(double2) * (size_t)K * N, hipMemcpyDeviceToDevice, st)) != hipSuccess)
+    return e;
+  if ((e = zgemm(0, 0, N, 1, M, mone, p.V, M, (long long)N * M, p.q0, 1, M, one, p.bvec, 1, N, K, st)) != hipSuccess)
+    return e;
+  // pack
+  if (p.pack32) {
+    const int nsl = (2 * p.MP) / 32 + (2 * p.NP) / 32;
+    hipLaunchKernelGGL(k_pack_f32, dim3(nsl, K), dim3(256), 0, st, M, N, p.MP, p.NP, p.has_mean, p.stride32, p.Linv,
+                       p.W, p.q0, p.bvec, p.pack32);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if (p.pack64) {
+    hipLaunchKernelGGL(k_pack_f64, dim3((2 * p.MP) / 16, K), dim3(64), 0, st, M, p.MP, p.has_mean, p.stride64, p.Linv,
+                       p.q0, p.pack64);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  return hipSuccess;
+}

@@ -1,0 +1,301 @@
+"""Drop-in estimator classes: ``Gmm_nbit`` / ``Gmm_quant`` / ``GaussianMixtureCplx``.
+
+Same constructor, attributes and estimate-side methods as the reference's
+``modules.gmm_cplx_bussgang.Gmm_nbit`` (gmm_cplx_bussgang.py:85-435) and
+``modules.gmm_cplx_quant.Gmm_quant`` (gmm_cplx_quant.py:85-457), so the experiment scripts'
+estimate loop (``mp_gmm(obj, *args)``, Bussgang_GMM.py:16-17, :284-289) runs unchanged.  All
+arithmetic of ``estimate_from_y`` / ``predict_proba_cplx`` / ``_predict_cplx`` runs in libqce.so
+on the GPU; this module only orchestrates and mirrors the reference's state mutations
+(``gm.means_``, ``gm.covariances_``, ``gm.precisions_cholesky_``, ``gm.n_features_in_`` become the
+observation-domain model of the last SNR, :262-313).
+
+The EM ``fit`` (training, :96-163, :437-848) is not on the estimate path; models come from a
+reference-fitted object (``from_reference``), from its attributes, or from ``from_params``.
+"""
+import copy
+import numbers
+
+import numpy as np
+
+from . import _lib
+
+try:  # the reference keeps its hyper-parameters and fitted weights in an sklearn object (:86-87)
+    from sklearn.mixture import GaussianMixture as _SkGaussianMixture
+except Exception:  # pragma: no cover - sklearn is part of the image
+    _SkGaussianMixture = None
+
+
+class _ParamBag:
+    """Minimal stand-in for sklearn's GaussianMixture when sklearn is not importable."""
+
+    def __init__(self, n_components=1, covariance_type="full", **kw):
+        self.n_components = n_components
+        self.covariance_type = covariance_type
+        for k, v in kw.items():
+            setattr(self, k, v)
+
+
+def _mode_of(n_summands_or_proba, K):
+    """Map the reference's mode argument (:197-242) to (mode, param).  Returns None for an empty
+    top-n selection (the reference divides by an empty sum -> NaN rows)."""
+    v = n_summands_or_proba
+    if isinstance(v, int):  # bool and int, exactly the reference's isinstance test (:197)
+        n = int(v)
+        if n < 0:  # idx_sort[:n] with negative n keeps K + n entries
+            n = max(K + n, 0)
+        if n == 0:
+            return None
+        return (_lib.MODE_TOPN, float(n))
+    if isinstance(v, str) and v == "all":
+        return (_lib.MODE_ALL, 0.0)
+    if isinstance(v, str):
+        raise ValueError(f"unsupported n_summands_or_proba {v!r}")
+    return (_lib.MODE_CUMP, float(v))  # floats and numpy integers take the probability branch (:229)
+
+
+def _nbits_of(n_bits):
+    if isinstance(n_bits, str):
+        raise NotImplementedError("n_bits must be a number or np.inf (the reference's prepare does not accept 'inf')")
+    return float(n_bits)
+
+
+class Gmm_nbit:
+    """Complex GMM with Bussgang-conditioned per-component LMMSE estimation on MI355X.
+
+    Mirrors ``Gmm_nbit`` (gmm_cplx_bussgang.py:85-94): ``gm`` is the sklearn GaussianMixture
+    parameter bag (``n_components``, ``covariance_type``, ``weights_`` ...), ``means_cplx``
+    (K,N) and ``covs_cplx`` (K,N,N) the channel-domain model.
+    """
+
+    def __init__(self, *gmm_args, device=0, **gmm_kwargs):
+        if _SkGaussianMixture is not None:
+            self.gm = _SkGaussianMixture(*gmm_args, **gmm_kwargs)
+        else:
+            self.gm = _ParamBag(*gmm_args, **gmm_kwargs)
+        self.means_cplx = None
+        self.covs_cplx = None
+        self.fft_covs = None
+        self.fft_means = None
+        self.chol = None
+        self.params = dict()
+        self.F2 = None
+        self.device = device
+        self.mirror_state = True
+        self._dev = None
+        self._dev_key = None
+        self._state = None  # "obs" after an observation-domain prepare, "chan" for the fit-state model
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def from_reference(cls, ref, device=0):
+        """Adopt a fitted reference ``Gmm_nbit``/``Gmm_quant`` (e.g. a joblib-loaded object,
+        Bussgang_GMM.py:270-278): reads means_cplx, covs_cplx and the sklearn parameter bag."""
+        obj = cls.__new__(cls)
+        Gmm_nbit.__init__(obj, device=device)
+        obj.gm = copy.deepcopy(ref.gm)
+        for name in ("means_cplx", "covs_cplx", "fft_covs", "fft_means", "chol", "F2"):
+            setattr(obj, name, copy.deepcopy(getattr(ref, name, None)))
+        obj.params = copy.deepcopy(getattr(ref, "params", {}))
+        return obj
+
+    @classmethod
+    def from_params(cls, means_cplx, covs_cplx, weights, covariance_type="full", device=0):
+        covs = np.asarray(covs_cplx, dtype=complex)
+        obj = cls(n_components=covs.shape[0], covariance_type=covariance_type, device=device)
+        obj.means_cplx = np.zeros(covs.shape[:2], complex) if means_cplx is None else np.asarray(means_cplx, complex)
+        obj.covs_cplx = covs
+        obj.gm.weights_ = np.asarray(weights, dtype=float)
+        obj.gm.means_ = obj.means_cplx.copy()
+        obj.gm.covariance_type = "full"
+        return obj
+
+    def fit(self, h, blocks=None, zero_mean=False):
+        """EM training (gmm_cplx_bussgang.py:96-163) is offline and outside the estimate path
+        this package accelerates."""
+        raise NotImplementedError("Gmm_nbit.fit is not provided by the MI355X estimate path; fit with the reference "
+                                  "and adopt the model with Gmm_nbit.from_reference(fitted)")
+
+    # ------------------------------------------------------------------ pickling (pool.starmap, :282-287)
+    def __getstate__(self):
+        d = self.__dict__.copy()
+        d["_dev"] = None
+        d["_dev_key"] = None
+        d["_state"] = None
+        return d
+
+    def __setstate__(self, d):
+        self.__dict__.update(d)
+
+    def __deepcopy__(self, memo):
+        cls = self.__class__
+        obj = cls.__new__(cls)
+        memo[id(self)] = obj
+        for k, v in self.__getstate__().items():
+            setattr(obj, k, copy.deepcopy(v, memo))
+        return obj
+
+    # ------------------------------------------------------------------ device model
+    def _device_model(self):
+        if self.covs_cplx is None:
+            raise ValueError("the model has no parameters (means_cplx / covs_cplx) yet")
+        if getattr(self.gm, "covariance_type", "full") != "full":
+            # every fit variant leaves covariance_type == 'full' (:116, :134, :144, :153); the
+            # reference raises for anything else (:316-317)
+            raise NotImplementedError(f"Estimation for covariance_type = {self.gm.covariance_type} is not implemented.")
+        covs = np.asarray(self.covs_cplx)
+        means = self.means_cplx
+        w = np.asarray(self.gm.weights_, dtype=float)
+        key = (id(self.covs_cplx), id(means), id(self.gm.weights_), covs.shape, self.device)
+        if self._dev is None or self._dev_key != key:
+            self._dev = _lib.DeviceModel(means, covs, w, device=self.device)
+            self._dev_key = key
+            self._state = None
+        return self._dev
+
+    def _mirror(self, dev, M):
+        """Reproduce the reference's mutation of ``self.gm`` (:262-264, :288, :309-313)."""
+        if not self.mirror_state:
+            return
+        t = dev.tables()
+        self.gm.means_ = t["means_y"]
+        self.gm.covariances_ = t["Cr"]
+        self.gm.precisions_cholesky_ = t["P"]
+        self.gm.n_features_in_ = M
+
+    def _prepare(self, A, snr_dB, n_bits, quantizer_type, quantizer, allow_inf=True):
+        dev = self._device_model()
+        nb = _nbits_of(n_bits)
+        qkind, thr, lab = _lib.QUANT_UNIFORM, None, None
+        if nb != 1 and not np.isinf(nb):
+            if quantizer_type == "uniform":
+                qkind = _lib.QUANT_UNIFORM
+            elif quantizer_type == "lloyd":
+                qkind = _lib.QUANT_LLOYD
+                if quantizer is None or quantizer[0] is None:
+                    raise ValueError("lloyd quantizer needs (thresholds, labels, rho)")
+                thr, lab = np.asarray(quantizer[0], float), np.asarray(quantizer[1], float)
+            else:
+                qkind = _lib.QUANT_OTHER
+        if np.isinf(nb) and not allow_inf and quantizer_type == "lloyd":
+            raise OverflowError("cannot convert float infinity to integer")
+        dev.prepare(A, snr_dB, nb, qkind, thr, lab)
+        self._state = "obs"
+        return dev
+
+    def _ensure_state(self):
+        """Device model matching the current ``gm`` state: after an estimate it is the
+        observation-domain model; before, the channel-domain model of the fit, which equals the
+        prepare with A = I, sigma^2 = 0 and no quantisation (Cr = C)."""
+        dev = self._device_model()
+        if self._state is None:
+            dev.prepare(None, float("inf"), float("inf"))
+            self._state = "chan"
+        return dev
+
+    # ------------------------------------------------------------------ reference API
+    def estimate_from_y(self, y, snr_dB, n_antennas, A=None, n_summands_or_proba=1, n_bits=1,
+                        quantizer_type="uniform", quantizer=None):
+        """gmm_cplx_bussgang.py:166-243 — returns h_est (B, N) complex128."""
+        y = np.asarray(y)
+        if y.ndim != 2:
+            raise ValueError("y must be a 2D array (B, M)")  # the reference fails at :405 for 1-D y
+        N = self.covs_cplx.shape[-1]
+        if A is not None:
+            A = np.asarray(A)
+            if A.shape[0] == A.shape[1] and np.array_equal(A, np.eye(A.shape[0])):
+                A = None  # identity: same arithmetic, fast path
+        elif n_antennas != N:
+            raise ValueError(f"n_antennas={n_antennas} does not match the model dimension {N}")
+        dev = self._prepare(A, snr_dB, n_bits, quantizer_type, quantizer, allow_inf=self._allow_inf())
+        M = dev.M
+        if self.mirror_state:
+            self._mirror(dev, M)
+        mode = _mode_of(n_summands_or_proba, dev.K)
+        B = y.shape[0]
+        if mode is None:
+            return np.full((B, N), np.nan + 0j)
+        yc = np.ascontiguousarray(y, dtype=np.complex128)
+        return dev.estimate(yc, mode[0], mode[1])
+
+    def _allow_inf(self):
+        return True
+
+    def _predict_cplx(self, X):
+        """gmm_cplx_bussgang.py:335-349."""
+        dev = self._ensure_state()
+        return dev.log_prob(X, want_lp=False, want_labels=True)[2]
+
+    def predict_proba_cplx(self, X):
+        """gmm_cplx_bussgang.py:351-367."""
+        dev = self._ensure_state()
+        return dev.log_prob(X, want_lp=False, want_proba=True)[1]
+
+    def _estimate_weighted_log_prob(self, X):
+        """gmm_cplx_bussgang.py:369-380."""
+        dev = self._ensure_state()
+        return dev.log_prob(X)[0]
+
+    def _estimate_log_weights(self):
+        """gmm_cplx_bussgang.py:382-383."""
+        return np.log(self.gm.weights_)
+
+    def _estimate_log_prob(self, X):
+        """gmm_cplx_bussgang.py:385-386 (weighted minus log weights)."""
+        return self._estimate_weighted_log_prob(X) - self._estimate_log_weights()
+
+    def _estimate_log_prob_resp(self, X):
+        """gmm_cplx_bussgang.py:632-656."""
+        wlp = self._estimate_weighted_log_prob(X)
+        from scipy.special import logsumexp
+        norm = logsumexp(wlp, axis=1)
+        with np.errstate(under="ignore"):
+            return norm, wlp - norm[:, None]
+
+
+class Gmm_quant(Gmm_nbit):
+    """Estimate side of ``Gmm_quant`` (gmm_cplx_quant.py:85-457): same tables and arithmetic as
+    ``Gmm_nbit`` (verified bit-identical).  Its prepare has no n_bits = inf
+    branch (:300-327): inf goes through the uniform-quantiser gain, which is the identity, so the
+    result is the same; with a Lloyd quantiser the reference overflows, which is mirrored."""
+
+    def __init__(self, *gmm_args, device=0, **gmm_kwargs):
+        super().__init__(*gmm_args, device=device, **gmm_kwargs)
+        self.quantizer = None
+        self.sigma2 = None
+        self.n_bits = None
+        self.quant_type = None
+        self.covariances_quant = None
+        self.eval_mode = False
+        self.precisions_cholesky_quant = None
+
+    def fit(self, h, n_bits, sigma2, quantizer, quant_type, blocks=None, zero_mean=False):
+        raise NotImplementedError("Gmm_quant.fit (EM with covariance recovery) is outside the MI355X estimate path; "
+                                  "fit with the reference and adopt the model with Gmm_quant.from_reference(fitted)")
+
+    def _allow_inf(self):
+        return False
+
+    def estimate_from_y(self, y, snr_dB, n_antennas, A=None, n_summands_or_proba=1, n_bits=1,
+                        quantizer_type="uniform", quantizer=None):
+        self.eval_mode = True  # gmm_cplx_quant.py:214
+        return super().estimate_from_y(y, snr_dB, n_antennas, A, n_summands_or_proba, n_bits, quantizer_type,
+                                       quantizer)
+
+
+class GaussianMixtureCplx(Gmm_nbit):
+    """The API name used by the project brief: ``estimate`` = ``estimate_from_y``,
+    ``predict_proba`` = ``predict_proba_cplx``, ``predict`` = ``_predict_cplx``."""
+
+    def estimate(self, *args, **kwargs):
+        return self.estimate_from_y(*args, **kwargs)
+
+    def predict_proba(self, X):
+        return self.predict_proba_cplx(X)
+
+    def predict(self, X):
+        return self._predict_cplx(X)
+
+
+def mp_gmm(obj, *args):
+    """The reference's pool worker (Bussgang_GMM.py:16-17)."""
+    return obj.estimate_from_y(*args)
