@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Throughput of the MI355X Bussgang-GMM estimate path (BASELINE.json metric).
+
+A step is one ``estimate_from_y`` of the reference (gmm_cplx_bussgang.py:166-243) over one batch:
+the per-SNR FP64 precompute (prepare) followed by the fused estimate kernel, with the batch of
+quantised observations already resident in HBM.  Default workload = the metric configuration
+(SURVEY.md §8(d) D2): K=128 components, N=M=64 antennas, 'full' covariances, 1-bit uniform
+quantiser, SNR 5 dB, mode 'all', B=100,000 observations per GPU.
+
+  python bench.py [--gpus N --steps K --warmup W] [--config metric|cfg1|cfg2|cfg4] [--shard batch|k]
+
+Multi-GPU (launched by torch.distributed.run, one rank per GPU): ``--shard batch`` (default) gives
+every rank its own B observations and the whole mixture (no data-path collective, weak scaling);
+``--shard k`` splits the K components over the ranks and combines with one RCCL all-reduce
+(strong scaling).  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "channel estimates/sec + MSE vs reference; K=128 N=64 full-cov, 1/2/4/8 GPU"
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
+
+CONFIGS = {
+    "metric": dict(K=128, N=64, cov="full", n_bits=1, qtype="uniform", B=100_000, snr=5.0),
+    "cfg1": dict(K=16, N=32, cov="full", n_bits=1, qtype="uniform", B=1_000, snr=5.0),
+    "cfg2": dict(K=64, N=64, cov="full", n_bits=1, qtype="uniform", B=10_000, snr=5.0),
+    "cfg3dense": dict(K=128, N=64, cov="circulant", n_bits=3, qtype="lloyd", B=100_000, snr=5.0),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0, help="override B (observations per GPU)")
+    ap.add_argument("--shard", default="batch", choices=["batch", "k"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_metric.json"),
+                    help="JSON with PMC-derived HBM bytes per launch of the estimate kernel")
+    return ap.parse_args()
+
+
+def make_inputs(cfg, seed, pool=2048):
+    """Synthetic batch of the configured shape: SCM channels (a seeded pool of `pool` distinct
+    channels, reused with fresh noise) -> quantised observations y = Q(h + n)."""
+    from quantized_channel_estimation_amd import inputs
+    K, N, B = cfg["K"], cfg["N"], cfg["B"]
+    means, covs, w = inputs.synthetic_model(K, N, cov_type=cfg["cov"], blocks=cfg.get("blocks"))
+    rng = np.random.default_rng(1000 + seed)
+    hp, _ = inputs.scm_generate(min(pool, B), 1, N, rng, n_path=3)
+    hp = hp[:, 0, :].astype(np.complex128)
+    h = hp[rng.integers(0, hp.shape[0], size=B)]
+    quantizer = (None, None, None)
+    if cfg["n_bits"] not in (1, np.inf):
+        quantizer = inputs.get_quantizer([cfg["snr"]], cfg["n_bits"], cfg["qtype"])[cfg["snr"]]
+    y = inputs.get_observation_nbit(h, cfg["snr"], None, cfg["n_bits"], quantizer[0], quantizer[1],
+                                    rng=np.random.default_rng(2000 + seed))
+    return means, covs, w, h, np.ascontiguousarray(y, dtype=np.complex128), quantizer
+
+
+def cpu_baseline(cfg, means, covs, w, y, quantizer, budget_s):
+    """Loop-faithful oracle (the reference's per-(sample, component) op order) on a bounded
+    sample of the same workload, single thread."""
+    from oracle import qce_oracle as O
+    try:
+        from threadpoolctl import threadpool_limits
+        lim = threadpool_limits(limits=1)
+    except Exception:  # pragma: no cover
+        lim = None
+    N = cfg["N"]
+    def run(n):
+        t0 = time.perf_counter()
+        O.estimate_loop(means, covs, w, y[:n], cfg["snr"], N, None, cfg["n_bits"], cfg["qtype"], quantizer)
+        return time.perf_counter() - t0
+    t1, t2 = run(4), run(36)
+    per = max((t2 - t1) / 32.0, 1e-6)
+    prep = max(t1 - 4 * per, 0.0)
+    n = int(max(16, min(y.shape[0], (budget_s - prep) / per)))
+    t0 = time.perf_counter()
+    O.estimate_loop(means, covs, w, y[:n], cfg["snr"], N, None, cfg["n_bits"], cfg["qtype"], quantizer)
+    dt = time.perf_counter() - t0
+    if lim is not None:
+        lim.unregister()
+    return dict(value=n / dt, unit="estimates/s", cores=1, kind="port",
+                sample=f"{n} observations of the same workload through oracle.estimate_loop (per-call prepare "
+                       f"included, 1 BLAS thread), {dt:.1f} s")
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from quantized_channel_estimation_amd import _lib
+    from quantized_channel_estimation_amd.sharding import ComponentShardEstimator, component_slices
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    cfg = dict(CONFIGS[args.config])
+    if args.batch:
+        cfg["B"] = args.batch
+    K, N, B = cfg["K"], cfg["N"], cfg["B"]
+    data_seed = rank if args.shard == "batch" else 0
+    means, covs, w, h, y, quantizer = make_inputs(cfg, data_seed)
+    qkind = {"uniform": _lib.QUANT_UNIFORM, "lloyd": _lib.QUANT_LLOYD}[cfg["qtype"]]
+    thr, lab = (quantizer[0], quantizer[1]) if cfg["n_bits"] not in (1, np.inf) and cfg["qtype"] == "lloyd" else \
+        (None, None)
+
+    dev = torch.device("cuda", local)
+    yd = torch.from_numpy(y).to(dev)
+    out = torch.empty((B, N), dtype=torch.complex128, device=dev)
+    stream = torch.cuda.Stream(dev)  # a real (non-null) stream: the library launches on it, events time it
+    torch.cuda.set_stream(stream)
+    sptr = stream.cuda_stream
+
+    if args.shard == "batch":
+        model = _lib.DeviceModel(means, covs, w, device=local)
+
+        def step(ev=None):
+            model.prepare(None, cfg["snr"], cfg["n_bits"], qkind, thr, lab, stream=sptr)
+            if ev is not None:
+                ev[0].record(stream)
+            model.estimate(yd, _lib.MODE_ALL, 0.0, out=out, stream=sptr)
+            if ev is not None:
+                ev[1].record(stream)
+            return out
+    else:
+        shard = ComponentShardEstimator(means, covs, w, rank, world, device=local)
+        m_b = torch.empty(B, dtype=torch.float64, device=dev)
+        s_b = torch.empty(B, dtype=torch.float64, device=dev)
+        a_b = torch.empty((B, 2 * N), dtype=torch.float32, device=dev)
+        from quantized_channel_estimation_amd.sharding import combine_partials_dist
+
+        def step(ev=None):
+            shard.prepare(None, cfg["snr"], cfg["n_bits"], qkind, thr, lab, stream=sptr)
+            if ev is not None:
+                ev[0].record(stream)
+            shard.dev.partial(yd, m_b, s_b, a_b, stream=sptr)
+            if ev is not None:
+                ev[1].record(stream)
+            return combine_partials_dist(m_b, s_b, a_b, shard.shift, N)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        res = step(events[i])
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    ms_per_step = elapsed / args.steps * 1e3
+    total_units = B * world if args.shard == "batch" else B
+    value = total_units * args.steps / elapsed
+
+    # parity + MSE of this rank's last result against the FP64 oracle on a subset
+    parity = None
+    mse = None
+    if rank == 0:
+        hg = res.cpu().numpy()
+        mse = float(np.mean(np.abs(hg - h) ** 2))
+        if not args.no_parity:
+            from oracle import qce_oracle as O
+            n_chk = min(B, 512)
+            ho = O.estimate(means, covs, w, y[:n_chk], cfg["snr"], N, None, "all", cfg["n_bits"], cfg["qtype"],
+                            quantizer)
+            parity = dict(samples=n_chk,
+                          rel_fro=float(np.linalg.norm(hg[:n_chk] - ho) / np.linalg.norm(ho)),
+                          mse_gpu=float(np.mean(np.abs(hg[:n_chk] - h[:n_chk]) ** 2)),
+                          mse_oracle=float(np.mean(np.abs(ho - h[:n_chk]) ** 2)))
+
+    # roofline of the dominant kernel (the fused estimate kernel)
+    k_local = K if args.shard == "batch" else (lambda s: s[1] - s[0])(component_slices(K, world)[rank])
+    flops_per_launch = 16.0 * k_local * N * N * B  # 16 K M N real flops / estimate
+    achieved = flops_per_launch / (kern_ms * 1e-3) / 1e12
+    traffic = None
+    if os.path.exists(args.traffic):
+        try:
+            tj = json.load(open(args.traffic))
+            if tj.get("config") == args.config and tj.get("B") == B:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
+                    frac=round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), traffic=traffic,
+                    kernel="k_est_all_f32" if args.shard == "batch" else "k_est_all_f32<PARTIAL>",
+                    kernel_ms=round(kern_ms, 4), flops_per_launch=flops_per_launch)
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(cfg, means, covs, w, y, quantizer, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "channel estimates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak" if args.shard == "batch" else "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: SCM-Toeplitz covariances (seeded), SCM channel pool + fresh CN noise, 1-bit quantised",
+            "config": {"workload": f"estimate_from_y K={K} N=M={N} cov={cfg['cov']} n_bits={cfg['n_bits']} "
+                                   f"{cfg['qtype']} snr={cfg['snr']}dB mode=all B={B}/GPU prepare-per-step",
+                       "K": K, "N": N, "B_per_gpu": B, "shard": args.shard,
+                       "parallelism": f"{args.shard}{world}"},
+            "mse": mse,
+            "parity": parity,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -65,9 +65,11 @@ int qce_model_destroy(qce_model* model);
  * A: (M,N) c128 observation matrix, or NULL for the identity (estimate_from_y :191-192).
  * n_bits: 1..8 or +INFINITY (np.inf).  thresholds (2^b-1) / labels (2^b) are the quantiser
  * tables of the lloyd kind (lloyd_max_quantizer.py:24-37); NULL otherwise.
+ * Runs on `stream` (NULL = the model's stream; pass the stream later estimates use so a prepare never
+ * overwrites tables an in-flight estimate still reads) and synchronises it to read the Cholesky status.
  * Returns QCE_ECHOL if some Cr_k is not positive definite (:43-46). */
 int qce_prepare(qce_model* model, const double* A, int M, double snr_db, double n_bits, int quant_kind,
-                const double* thresholds, const double* labels, int n_levels);
+                const double* thresholds, const double* labels, int n_levels, void* stream);
 
 /* Channel estimates: `estimate_from_y` (gmm_cplx_bussgang.py:166-243) for y (B,M) c128 -> h (B,N) c128.
  * mode/mode_param: QCE_MODE_ALL; QCE_MODE_TOPN with n; QCE_MODE_CUMP with p. */

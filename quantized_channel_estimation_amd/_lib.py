@@ -30,7 +30,7 @@ SIGNATURES = {
                                         ctypes.POINTER(_vp)]),
     "qce_model_destroy": (ctypes.c_int, [_vp]),
     "qce_prepare": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int, _vp, _vp,
-                                   ctypes.c_int]),
+                                   ctypes.c_int, _vp]),
     "qce_estimate": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, _vp, ctypes.c_int, _vp]),
     "qce_log_prob": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int, _vp]),
     "qce_estimate_partial": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int, _vp]),
@@ -131,7 +131,7 @@ class DeviceModel:
         except Exception:
             pass
 
-    def prepare(self, A, snr_db, n_bits, quant_kind=QUANT_UNIFORM, thresholds=None, labels=None):
+    def prepare(self, A, snr_db, n_bits, quant_kind=QUANT_UNIFORM, thresholds=None, labels=None, stream=None):
         lib = load()
         if A is None:
             M, a = self.N, None
@@ -147,7 +147,7 @@ class DeviceModel:
             thr = np.ascontiguousarray(thresholds, dtype=np.float64)
             nlev = lab.size
         check(lib.qce_prepare(self._h, ptr(a), int(M), float(snr_db), float(n_bits), int(quant_kind), ptr(thr),
-                              ptr(lab), int(nlev)))
+                              ptr(lab), int(nlev), stream))
         self.M = M
 
     def estimate(self, y, mode=MODE_ALL, param=0.0, out=None, stream=None):

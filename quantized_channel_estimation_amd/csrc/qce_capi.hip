@@ -210,7 +210,7 @@ int qce_model_destroy(qce_model* m) {
 }
 
 int qce_prepare(qce_model* m, const double* A, int M, double snr_db, double n_bits, int quant_kind,
-                const double* thresholds, const double* labels, int n_levels) {
+                const double* thresholds, const double* labels, int n_levels, void* stream) {
   int rc = check_model(m, false);
   if (rc) return rc;
   const int N = m->N, K = m->K;
@@ -234,7 +234,7 @@ int qce_prepare(qce_model* m, const double* A, int M, double snr_db, double n_bi
       return fail(QCE_EARG, "lloyd quantiser needs 2^b labels and 2^b-1 thresholds");
   }
   DeviceGuard g(m->device);
-  hipStream_t st = m->stream;
+  hipStream_t st = pick_stream(m, stream);
   const size_t KMM = (size_t)K * M * M, KMN = (size_t)K * M * N;
   HIPCHK(m->A.ensure((size_t)M * N));
   HIPCHK(m->Cy.ensure(KMM));

@@ -91,10 +91,10 @@ class ComponentShardEstimator:
         self.group = group
         self.shift = None
 
-    def prepare(self, A, snr_db, n_bits, quant_kind=_lib.QUANT_UNIFORM, thresholds=None, labels=None):
+    def prepare(self, A, snr_db, n_bits, quant_kind=_lib.QUANT_UNIFORM, thresholds=None, labels=None, stream=None):
         import torch
         import torch.distributed as dist
-        self.dev.prepare(A, snr_db, n_bits, quant_kind, thresholds, labels)
+        self.dev.prepare(A, snr_db, n_bits, quant_kind, thresholds, labels, stream=stream)
         c = self.dev.tables()["cconst"]
         dev = torch.device("cuda", self.dev.device) if torch.cuda.is_available() else torch.device("cpu")
         t = torch.tensor([float(np.max(c))], dtype=torch.float64, device=dev)
