@@ -3,6 +3,7 @@
 // HIP stream per model.
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -77,6 +78,14 @@ struct qce_model {
   DevBuf<double> lp_scr, proba_scr, m_scr, s_scr;
   DevBuf<float> w_scr, acc_scr;
   DevBuf<long long> lab_scr;
+  // FP16 two-term split tables (qce_estimate_h2.hip)
+  DevBuf<char> pack16;
+  DevBuf<float> sinv;
+  long long cstride16 = 0;
+  double y_scale = 1.0;
+  DevBuf<double> sp_m, sp_s;
+  DevBuf<float> sp_a;
+  int cu_count = 256;
 };
 
 namespace {
@@ -121,6 +130,68 @@ int stage_input(qce_model* m, const double* y, long long B, int io, hipStream_t 
   HIPCHK(m->y_scr.ensure((size_t)B * m->M));
   HIPCHK(hipMemcpyAsync(m->y_scr.p, y, sizeof(double2) * (size_t)B * m->M, hipMemcpyHostToDevice, st));
   *dy = m->y_scr.p;
+  return QCE_OK;
+}
+
+bool use_h2() {
+  const char* e = getenv("QCE_KERNEL");
+  return !(e && strcmp(e, "f32") == 0);
+}
+
+// split-K factor that balances ceil(B/256) workgroups over the resident slots
+int choose_nsplit(qce_model* m, long long B) {
+  const char* e = getenv("QCE_NSPLIT");
+  if (e && atoi(e) > 0) return atoi(e) < m->K ? atoi(e) : m->K;
+  const long long tiles = (B + 255) / 256;
+  const long long slots = (long long)m->cu_count * qce_h2_blocks_per_cu(m->MP, m->NP, m->has_mean);
+  auto eff = [&](int s) {
+    const long long u = tiles * s;
+    return (double)u / (double)(slots * ((u + slots - 1) / slots));
+  };
+  int best = 1;
+  double be = eff(1);
+  const int smax = m->K / 8 < 8 ? (m->K / 8 < 1 ? 1 : m->K / 8) : 8;
+  for (int s = 2; s <= smax; ++s)
+    if (eff(s) > be + 0.03) {
+      be = eff(s);
+      best = s;
+    }
+  return best;
+}
+
+QceH2Args h2_args(qce_model* m, const double2* y, long long B, int nsplit) {
+  QceH2Args a;
+  a.B = B;
+  a.M = m->M;
+  a.N = m->N;
+  a.K = m->K;
+  a.MP = m->MP;
+  a.NP = m->NP;
+  a.has_mean = m->has_mean;
+  a.nsplit = nsplit;
+  a.y_scale = m->y_scale;
+  a.y = y;
+  a.pack = m->pack16.p;
+  a.cstride = m->cstride16;
+  a.sinv = m->sinv.p;
+  a.cconst = m->cconst.p;
+  return a;
+}
+
+// 'all' mode on the FP16 split kernel: final h, or the (m, s, acc) partial when h == nullptr
+int run_h2(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, float* oa,
+           hipStream_t st) {
+  const int nsplit = choose_nsplit(m, B);
+  QceH2Args a = h2_args(m, dy, B, nsplit);
+  if (nsplit == 1) {
+    HIPCHK(qce_launch_est_h2(a, h, om, os, oa, h == nullptr, st));
+    return QCE_OK;
+  }
+  HIPCHK(m->sp_m.ensure((size_t)nsplit * B));
+  HIPCHK(m->sp_s.ensure((size_t)nsplit * B));
+  HIPCHK(m->sp_a.ensure((size_t)nsplit * B * 2 * m->N));
+  HIPCHK(qce_launch_est_h2(a, nullptr, m->sp_m.p, m->sp_s.p, m->sp_a.p, true, st));
+  HIPCHK(qce_launch_merge_splits(B, m->N, nsplit, m->sp_m.p, m->sp_s.p, m->sp_a.p, h, om, os, oa, st));
   return QCE_OK;
 }
 
@@ -173,6 +244,9 @@ int qce_model_create(int K, int N, const double* means_cplx, const double* covs_
         break;
       }
   }
+  if (hipDeviceGetAttribute(&m->cu_count, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      m->cu_count < 1)
+    m->cu_count = 256;
   hipError_t e = hipStreamCreateWithFlags(&m->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = m->means.ensure((size_t)K * N);
   if (e == hipSuccess) e = m->covs.ensure((size_t)K * N * N);
@@ -204,6 +278,11 @@ int qce_model_destroy(qce_model* m) {
   m->w_scr.release();
   m->acc_scr.release();
   m->lab_scr.release();
+  m->pack16.release();
+  m->sinv.release();
+  m->sp_m.release();
+  m->sp_s.release();
+  m->sp_a.release();
   if (m->stream) (void)hipStreamDestroy(m->stream);
   delete m;
   return QCE_OK;
@@ -327,6 +406,19 @@ int qce_prepare(qce_model* m, const double* A, int M, double snr_db, double n_bi
   p.pack64 = m->pack64.p;
   p.stride64 = s64;
   HIPCHK(qce_launch_prepare(p, st));
+  // FP16 two-term split tables; the observation scale makes quantiser outputs exact in fp16
+  // (1 bit: y sqrt(2) = +-1; uniform: y 2/delta = odd integers), folded into the slice scales
+  double y_scale = 1.0;
+  if (kind == 0) y_scale = sqrt(2.0);
+  else if (kind == 1 && quant_kind == QCE_QUANT_UNIFORM && delta > 0.0) y_scale = 2.0 / delta;
+  const long long cs16 = qce_pack_h2_stride_bytes(MP, NP, m->has_mean);
+  const int nslices = (2 * MP) / 32 + (2 * NP) / 32;
+  HIPCHK(m->pack16.ensure((size_t)cs16 * K));
+  HIPCHK(m->sinv.ensure((size_t)nslices * K));
+  HIPCHK(qce_launch_pack_h2(K, M, N, MP, NP, m->has_mean, cs16, y_scale, m->Linv.p, m->W.p, m->q0.p, m->bvec.p,
+                            m->pack16.p, m->sinv.p, st));
+  m->cstride16 = cs16;
+  m->y_scale = y_scale;
   std::vector<int> status(K);
   HIPCHK(hipMemcpyAsync(status.data(), m->status.p, sizeof(int) * K, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
@@ -366,7 +458,11 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
   }
   QceEstArgs a = est_args(m, dy, B);
   if (mode == QCE_MODE_ALL) {
-    HIPCHK(qce_launch_est_all(a, dh, st));
+    if (use_h2()) {
+      if ((rc = run_h2(m, dy, B, dh, nullptr, nullptr, nullptr, st))) return rc;
+    } else {
+      HIPCHK(qce_launch_est_all(a, dh, st));
+    }
   } else {
     int kmode, n = 0;
     double p = 0.0;
@@ -452,8 +548,12 @@ int qce_estimate_partial(qce_model* m, const double* y, int64_t B, double* m_out
     ds = m->s_scr.p;
     da = m->acc_scr.p;
   }
-  QceEstArgs a = est_args(m, dy, B);
-  HIPCHK(qce_launch_est_partial(a, dm, ds, da, st));
+  if (use_h2()) {
+    if ((rc = run_h2(m, dy, B, nullptr, dm, ds, da, st))) return rc;
+  } else {
+    QceEstArgs a = est_args(m, dy, B);
+    HIPCHK(qce_launch_est_partial(a, dm, ds, da, st));
+  }
   if (io == QCE_IO_HOST) {
     HIPCHK(hipMemcpyAsync(m_out, dm, sizeof(double) * B, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(s_out, ds, sizeof(double) * B, hipMemcpyDeviceToHost, st));

@@ -202,3 +202,55 @@ def test_device_io_torch():
     out = dm.estimate(yd)
     dm.synchronize()
     assert rel_fro(out.cpu().numpy(), host) == 0.0
+
+
+@pytest.mark.parametrize("env", [{}, {"QCE_NSPLIT": "1"}, {"QCE_NSPLIT": "3"}, {"QCE_NSPLIT": "7"},
+                                 {"QCE_KERNEL": "f32"}])
+def test_all_mode_kernel_variants_vs_oracle(env, monkeypatch):
+    """FP16 two-term split kernel (default), its split-K merge, and the FP32-MFMA kernel all
+    agree with the FP64 oracle."""
+    _gpu_or_skip()
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import Gmm_nbit
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    K, N, B = 64, 64, 3000
+    means, covs, w, h, y, qz = _synthetic(K, N, B, 21, 1, mean=True)
+    g = Gmm_nbit.from_params(means, covs, w)
+    hg = g.estimate_from_y(y, 5.0, N, None, "all", 1)
+    ho = O.estimate(means, covs, w, y, 5.0, N, None, "all", 1)
+    assert rel_fro(hg, ho) < H_TOL, rel_fro(hg, ho)
+
+
+@pytest.mark.parametrize("n_bits,snr", [(1, -10.0), (1, 20.0), (2, 5.0), (np.inf, 10.0)])
+def test_inexact_observations_take_the_precise_path(n_bits, snr):
+    """Observations that are not quantiser outputs (here: raw y declared as 1-bit / 2-bit) are not
+    exact in fp16; the kernel detects that per wave and splits y too — results stay within tolerance."""
+    _gpu_or_skip()
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import Gmm_nbit, inputs
+    K, N, B = 48, 32, 1500
+    means, covs, w = inputs.synthetic_model(K, N, seed=9)
+    rng = np.random.default_rng(10)
+    h, _ = inputs.scm_generate(B, 1, N, rng, n_path=3)
+    y = h[:, 0, :].astype(complex) + 10 ** (-snr / 20) * inputs.crandn(B, N, rng=rng)  # unquantised
+    qz = (None, None, None)
+    if n_bits == 2:
+        qz = inputs.uniform_quantizer(snr, 2)
+    g = Gmm_nbit.from_params(means, covs, w)
+    hg = g.estimate_from_y(y, snr, N, None, "all", n_bits, "uniform", qz)
+    ho = O.estimate(means, covs, w, y, snr, N, None, "all", n_bits, "uniform", qz)
+    assert rel_fro(hg, ho) < H_TOL, rel_fro(hg, ho)
+
+
+def test_ragged_and_tiny_batches():
+    _gpu_or_skip()
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import Gmm_nbit
+    K, N = 20, 24
+    means, covs, w, h, y, qz = _synthetic(K, N, 600, 33, 1)
+    g = Gmm_nbit.from_params(means, covs, w)
+    for B in (1, 2, 31, 255, 256, 257, 511, 600):
+        hg = g.estimate_from_y(y[:B], 5.0, N, None, "all", 1)
+        ho = O.estimate(means, covs, w, y[:B], 5.0, N, None, "all", 1)
+        assert rel_fro(hg, ho) < H_TOL, (B, rel_fro(hg, ho))
