@@ -28,6 +28,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "channel estimates/sec + MSE vs reference; K=128 N=64 full-cov, 1/2/4/8 GPU"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
+FP16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense FP16/BF16 MFMA (spec, no sparsity)
 
 CONFIGS = {
     "metric": dict(K=128, N=64, cov="full", n_bits=1, qtype="uniform", B=100_000, snr=5.0),
@@ -194,22 +195,31 @@ def main():
                           mse_gpu=float(np.mean(np.abs(hg[:n_chk] - h[:n_chk]) ** 2)),
                           mse_oracle=float(np.mean(np.abs(ho - h[:n_chk]) ** 2)))
 
-    # roofline of the dominant kernel (the fused estimate kernel)
+    # roofline of the dominant kernel (the fused estimate kernel + its stream-K merge)
     k_local = K if args.shard == "batch" else (lambda s: s[1] - s[0])(component_slices(K, world)[rank])
-    flops_per_launch = 16.0 * k_local * N * N * B  # 16 K M N real flops / estimate
+    flops_per_launch = 16.0 * k_local * N * N * B  # 16 K M N real flops / estimate (algorithmic)
     achieved = flops_per_launch / (kern_ms * 1e-3) / 1e12
+    f32_kernel = os.environ.get("QCE_KERNEL") == "f32"
+    peak = FP32_MFMA_PEAK_TFLOPS if f32_kernel else FP16_MFMA_PEAK_TFLOPS
+    # executed MFMA work: lower-triangular tiles of E(Linv) skipped (R/32 slices of 32x16 tiles) and,
+    # for the fp16 kernel, two products (hi, lo) per fp32-class MAC
+    nsl = (2 * N) // 32
+    tri = (sum(2 * r + 2 for r in range(nsl)) / (nsl * 2 * nsl) + 1.0) / 2.0
+    executed = flops_per_launch * tri * (1.0 if f32_kernel else 2.0)
     traffic = None
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
-            if tj.get("config") == args.config and tj.get("B") == B:
+            if tj.get("config") == args.config and tj.get("B") == B and tj.get("kernel") == ("f32" if f32_kernel else "h2"):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=FP32_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
-                    frac=round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), traffic=traffic,
-                    kernel="k_est_all_f32" if args.shard == "batch" else "k_est_all_f32<PARTIAL>",
-                    kernel_ms=round(kern_ms, 4), flops_per_launch=flops_per_launch)
+    roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=peak, unit="TFLOP/s",
+                    frac=round(achieved / peak, 4), traffic=traffic,
+                    kernel=("k_est_all_f32" if f32_kernel else "k_est_all_h2+k_merge_streamk"),
+                    peak_dtype="fp32 MFMA" if f32_kernel else "fp16 MFMA (dense)",
+                    kernel_ms=round(kern_ms, 4), flops_per_launch=flops_per_launch,
+                    mfma_issue_frac=round(executed / (kern_ms * 1e-3) / 1e12 / peak, 4))
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -227,7 +237,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if args.shard == "batch" else "strong",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if os.environ.get("QCE_KERNEL") == "f32" else "f16x2 (fp16 hi+lo split, fp32 accumulate, fp64 softmax)",
             "data": "synthetic: SCM-Toeplitz covariances (seeded), SCM channel pool + fresh CN noise, 1-bit quantised",
             "config": {"workload": f"estimate_from_y K={K} N=M={N} cov={cfg['cov']} n_bits={cfg['n_bits']} "
                                    f"{cfg['qtype']} snr={cfg['snr']}dB mode=all B={B}/GPU prepare-per-step",

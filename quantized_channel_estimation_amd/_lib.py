@@ -9,7 +9,7 @@ import os
 import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "libqce.so")
+LIB_PATH = os.environ.get("QCE_LIB") or os.path.join(_PKG, "libqce.so")  # QCE_LIB: diagnostic builds only
 
 QCE_OK, QCE_EARG, QCE_ECHOL, QCE_ENOTIMPL, QCE_EHIP, QCE_ESTATE = range(6)
 MODE_ALL, MODE_TOPN, MODE_CUMP = 0, 1, 2

@@ -34,16 +34,21 @@ def _newer(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(verbose=False, jobs=None):
+def build(verbose=False, jobs=None, variant=None):
+    """variant "stamps": diagnostic library libqce_stamps.so compiled with -DQCE_STAMPS."""
     hipcc = _hipcc()
-    os.makedirs(BUILD, exist_ok=True)
+    build_dir = BUILD if variant is None else BUILD + "_" + variant
+    lib_path = LIB if variant is None else os.path.join(PKG, f"libqce_{variant}.so")
+    os.makedirs(build_dir, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     headers = sorted(glob.glob(os.path.join(CSRC, "*.h"))) + [os.path.join(ROOT, "include", "qce.h")]
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result",
              "-I" + os.path.join(ROOT, "include")]
+    if variant == "stamps":
+        flags.append("-DQCE_STAMPS")
 
     def compile_one(src):
-        obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+        obj = os.path.join(build_dir, os.path.basename(src) + ".o")
         if _newer(obj, [src] + headers):
             cmd = [hipcc] + flags + ["-c", src, "-o", obj]
             if verbose:
@@ -55,15 +60,15 @@ def build(verbose=False, jobs=None):
 
     with cf.ThreadPoolExecutor(max_workers=jobs or min(8, len(srcs))) as ex:
         objs = list(ex.map(compile_one, srcs))
-    if _newer(LIB, objs):
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+    if _newer(lib_path, objs):
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path] + objs
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
-    return LIB
+    return lib_path
 
 
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
+    print(build(verbose="-v" in sys.argv, variant="stamps" if "--stamps" in sys.argv else None))

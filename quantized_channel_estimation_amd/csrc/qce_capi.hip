@@ -85,6 +85,7 @@ struct qce_model {
   double y_scale = 1.0;
   DevBuf<double> sp_m, sp_s;
   DevBuf<float> sp_a;
+  DevBuf<int> yflag;
   int cu_count = 256;
 };
 
@@ -138,28 +139,27 @@ bool use_h2() {
   return !(e && strcmp(e, "f32") == 0);
 }
 
-// split-K factor that balances ceil(B/256) workgroups over the resident slots
-int choose_nsplit(qce_model* m, long long B) {
-  const char* e = getenv("QCE_NSPLIT");
-  if (e && atoi(e) > 0) return atoi(e) < m->K ? atoi(e) : m->K;
+// 'all' mode on the FP16 split kernel, stream-K scheduled over the resident workgroups: final h,
+// or the (m, s, acc) partial when h == nullptr (K-shard path)
+int run_h2(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, float* oa,
+           hipStream_t st) {
   const long long tiles = (B + 255) / 256;
-  const long long slots = (long long)m->cu_count * qce_h2_blocks_per_cu(m->MP, m->NP, m->has_mean);
-  auto eff = [&](int s) {
-    const long long u = tiles * s;
-    return (double)u / (double)(slots * ((u + slots - 1) / slots));
-  };
-  int best = 1;
-  double be = eff(1);
-  const int smax = m->K / 8 < 8 ? (m->K / 8 < 1 ? 1 : m->K / 8) : 8;
-  for (int s = 2; s <= smax; ++s)
-    if (eff(s) > be + 0.03) {
-      be = eff(s);
-      best = s;
-    }
-  return best;
-}
-
-QceH2Args h2_args(qce_model* m, const double2* y, long long B, int nsplit) {
+  long long slots = (long long)m->cu_count * qce_h2_blocks_per_cu(m->MP, m->NP, m->has_mean);
+  const char* e = getenv("QCE_WORKGROUPS");
+  if (e && atoll(e) > 0) slots = atoll(e);
+  // data-parallel rounds of whole tiles, stream-K over the remaining tiles' (tile, component) items
+  long long nwg, R, L;
+  if (tiles >= slots) {
+    nwg = slots;
+    R = tiles / slots;
+    const long long tail_items = (tiles - R * slots) * m->K;
+    L = (tail_items + nwg - 1) / nwg;
+  } else {
+    R = 0;
+    L = (tiles * m->K + slots - 1) / slots;
+    if (L < 1) L = 1;
+    nwg = (tiles * m->K + L - 1) / L;
+  }
   QceH2Args a;
   a.B = B;
   a.M = m->M;
@@ -168,30 +168,28 @@ QceH2Args h2_args(qce_model* m, const double2* y, long long B, int nsplit) {
   a.MP = m->MP;
   a.NP = m->NP;
   a.has_mean = m->has_mean;
-  a.nsplit = nsplit;
+  a.nwg = (int)nwg;
+  a.R = (int)R;
+  a.L = L;
   a.y_scale = m->y_scale;
-  a.y = y;
+  a.y = dy;
   a.pack = m->pack16.p;
   a.cstride = m->cstride16;
   a.sinv = m->sinv.p;
   a.cconst = m->cconst.p;
-  return a;
-}
-
-// 'all' mode on the FP16 split kernel: final h, or the (m, s, acc) partial when h == nullptr
-int run_h2(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, float* oa,
-           hipStream_t st) {
-  const int nsplit = choose_nsplit(m, B);
-  QceH2Args a = h2_args(m, dy, B, nsplit);
-  if (nsplit == 1) {
-    HIPCHK(qce_launch_est_h2(a, h, om, os, oa, h == nullptr, st));
-    return QCE_OK;
-  }
-  HIPCHK(m->sp_m.ensure((size_t)nsplit * B));
-  HIPCHK(m->sp_s.ensure((size_t)nsplit * B));
-  HIPCHK(m->sp_a.ensure((size_t)nsplit * B * 2 * m->N));
-  HIPCHK(qce_launch_est_h2(a, nullptr, m->sp_m.p, m->sp_s.p, m->sp_a.p, true, st));
-  HIPCHK(qce_launch_merge_splits(B, m->N, nsplit, m->sp_m.p, m->sp_s.p, m->sp_a.p, h, om, os, oa, st));
+  a.h = h;
+  a.om = om;
+  a.os = os;
+  a.oa = oa;
+  HIPCHK(m->sp_m.ensure((size_t)nwg * 2 * 256));
+  HIPCHK(m->sp_s.ensure((size_t)nwg * 2 * 256));
+  HIPCHK(m->sp_a.ensure((size_t)nwg * 2 * 256 * 2 * m->N));
+  HIPCHK(m->yflag.ensure(1));
+  a.yflag = m->yflag.p;
+  a.pm = m->sp_m.p;
+  a.ps = m->sp_s.p;
+  a.pa = m->sp_a.p;
+  HIPCHK(qce_launch_est_h2(a, h == nullptr, st));
   return QCE_OK;
 }
 
@@ -283,6 +281,7 @@ int qce_model_destroy(qce_model* m) {
   m->sp_m.release();
   m->sp_s.release();
   m->sp_a.release();
+  m->yflag.release();
   if (m->stream) (void)hipStreamDestroy(m->stream);
   delete m;
   return QCE_OK;

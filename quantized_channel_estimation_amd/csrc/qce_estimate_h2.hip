@@ -11,16 +11,22 @@
 //    v_mfma_f32_32x32x16_f16 with fp32 accumulation — fp32-class results at 1/8 of the fp32-MFMA
 //    cycles.  Observations that are not exact (Lloyd-Max labels, n_bits = inf, or any unquantised
 //    input) are split too (y = y_hi + y_lo) and the wave takes a three-product path
-//    (a_hi y_hi + a_lo y_hi + a_hi y_lo); the choice is per wave, by ballot, so no input can
-//    silently lose precision;
+//    (a_hi y_hi + a_lo y_hi + a_hi y_lo); the choice is made per workgroup tile (any inexact
+//    sample), so no input can silently lose precision;
 //  * one 512-thread workgroup = 8 waves x 32 samples shares each component's tables through LDS:
 //    the Linv part (GL) and the W part (GW) have their own LDS slot and are streamed by
 //    global_load_lds (16 B per lane) one phase ahead of the MFMAs that read them;
-//  * the K loop can be split over blockIdx.y (split-K) to fill the chip when B/256 workgroups do
-//    not divide evenly over the CUs; split partials (running max, sum, accumulator) are merged by
-//    k_merge_splits — the same merge the K-shard multi-GPU path uses.
+//  * stream-K scheduling: the (sample tile, component) work items are dealt to exactly as many
+//    persistent workgroups as fit on the chip, L = ceil(tiles*K / P) consecutive items each, so
+//    every CU does the same work whatever B is.  A tile whose K range is cut between two
+//    workgroups leaves partials (running max, sum, accumulator) that k_merge_streamk combines —
+//    the same combine the K-shard multi-GPU path uses.
 #include "qce_common.h"
 #include "qce_kernels.h"
+
+#include <stdlib.h>
+
+#include <utility>
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
@@ -55,6 +61,7 @@ QCE_DEV f32x16 mfma_h(f16x8 a, f16x8 b, f32x16 c) { return __builtin_amdgcn_mfma
 // global -> LDS copy of `bytes` (multiple of 1 KB) by the 8 waves, one 1 KB wave-instruction each
 template <int BYTES>
 QCE_DEV void stage(const char* __restrict__ src, char* dst, int wave, int lane) {
+  wave = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: no waterfall around the M0 base
 #pragma unroll
   for (int c = wave; c < BYTES / 1024; c += 8) {
     __builtin_amdgcn_global_load_lds((const void*)(src + c * 1024 + lane * 16),
@@ -62,6 +69,300 @@ QCE_DEV void stage(const char* __restrict__ src, char* dst, int wave, int lane) 
   }
 }
 
+template <int N_>
+QCE_DEV void wait_vm() {
+  if constexpr (N_ == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N_ == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N_ == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N_ == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+  else if constexpr (N_ == 13) asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// barrier without the vmcnt(0) __syncthreads() would add (keeps prefetches in flight)
+#ifdef QCE_STAMPS
+// diagnostic build only (-DQCE_STAMPS): per-wave cycle sums of the deep loop's segments
+__device__ unsigned long long g_qce_stamps[4096 * 8 * 8];
+#define QCE_STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0;
+#define QCE_STAMP(i)                                                 \
+  do {                                                               \
+    __builtin_amdgcn_sched_barrier(0);                               \
+    unsigned long long t_;                                           \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    if ((i) >= 0) st_acc[(i)] += t_ - st_prev;                      \
+    st_prev = t_;                                                    \
+    __builtin_amdgcn_sched_barrier(0);                               \
+  } while (0)
+#define QCE_STAMP_FLUSH                                                                               \
+  if (lane == 0 && blockIdx.x < 4096)                                                                 \
+    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_qce_stamps[(blockIdx.x * 8 + wave) * 8 + i_], st_acc[i_]);
+#else
+#define QCE_STAMP_DECL
+#define QCE_STAMP(i)
+#define QCE_STAMP_FLUSH
+#endif
+
+QCE_DEV void raw_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+QCE_DEV int gl_slice_of(int idx, int hmi) {  // slice r holds steps [r(r+1) + hmi r, ... + 2r + 2 + hmi)
+  int r = 0, base = 0;
+  while (idx >= base + 2 * r + 2 + hmi) {
+    base += 2 * r + 2 + hmi;
+    ++r;
+  }
+  return r;
+}
+
+// GL phase: u = E(Linv)[y;1] slice by slice, quad = sum u^2 (FP64 across slices).  LDS fragments are
+// software-pipelined two k-steps ahead of the MFMAs that consume them.
+template <int MP, int NP, bool HM, bool Y2>
+QCE_DEV double gl_phase(const char* sl, const f16x8* yh, const f16x8* yl, const float* sk, int lane) {
+  // sk: this component's slice scales, already in registers (see CompScalars)
+  using G = H2Geom<MP, NP, HM>;
+  constexpr int NST = G::GL_STEPS;
+  constexpr bool PF = !Y2;  // the three-product path has no registers left for the prefetch ring
+  f16x8 ra[2], rb[2];
+  if (PF) {
+    ra[0] = lds_frag(sl, 0, lane);
+    rb[0] = lds_frag(sl, 1024, lane);
+    if (NST > 1) {
+      ra[1] = lds_frag(sl, 2048, lane);
+      rb[1] = lds_frag(sl, 3072, lane);
+    }
+  }
+  double quad = 0.0;
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+#pragma unroll
+  for (int idx = 0; idx < NST; ++idx) {
+    const int r = gl_slice_of(idx, G::HMI);
+    const int s = idx - G::gl_off(r);
+    f16x8 a0, a1;
+    if (PF) {
+      a0 = ra[idx & 1];
+      a1 = rb[idx & 1];
+      if (idx + 2 < NST) {
+        ra[idx & 1] = lds_frag(sl, (idx + 2) * 2048, lane);
+        rb[idx & 1] = lds_frag(sl, (idx + 2) * 2048 + 1024, lane);
+      }
+    } else {
+      a0 = lds_frag(sl, idx * 2048, lane);
+      a1 = lds_frag(sl, idx * 2048 + 1024, lane);
+    }
+    const bool mean_step = HM && s == 2 * r + 2;
+    const f16x8 yv = mean_step ? yh[G::KS] : yh[s < G::KS ? s : 0];
+    acc = mfma_h(a0, yv, acc);
+    acc = mfma_h(a1, yv, acc);
+    if (Y2 && !mean_step) acc = mfma_h(a0, yl[s < G::KS ? s : 0], acc);
+    if (s == 2 * r + 1 + G::HMI) {  // slice complete
+      float qs = 0.0f;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) qs = fmaf(acc[q], acc[q], qs);
+      const double is = (double)sk[r];
+      quad = fma((double)qs, is * is, quad);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+    }
+  }
+  return quad;
+}
+
+// GW phase over slices [R0, R1) held contiguously from `sw`: out = alpha out + p s_r Z_r.
+template <int MP, int NP, bool HM, bool Y2, int R0, int R1>
+QCE_DEV void gw_phase(const char* sw, const f16x8* yh, const f16x8* yl, const float* sk, float p, float alpha,
+                      f32x16* out, int lane) {
+  // sk: slice scales in registers
+  using G = H2Geom<MP, NP, HM>;
+  constexpr int SPS = G::KS + G::HMI;  // steps per slice
+  constexpr int NST = (R1 - R0) * SPS;
+  constexpr bool PF = !Y2;
+  f16x8 ra[2], rb[2];
+  if (PF) {
+    ra[0] = lds_frag(sw, 0, lane);
+    rb[0] = lds_frag(sw, 1024, lane);
+    if (NST > 1) {
+      ra[1] = lds_frag(sw, 2048, lane);
+      rb[1] = lds_frag(sw, 3072, lane);
+    }
+  }
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+#pragma unroll
+  for (int idx = 0; idx < NST; ++idx) {
+    const int r = R0 + idx / SPS, s = idx % SPS;
+    f16x8 a0, a1;
+    if (PF) {
+      a0 = ra[idx & 1];
+      a1 = rb[idx & 1];
+      if (idx + 2 < NST) {
+        ra[idx & 1] = lds_frag(sw, (idx + 2) * 2048, lane);
+        rb[idx & 1] = lds_frag(sw, (idx + 2) * 2048 + 1024, lane);
+      }
+    } else {
+      a0 = lds_frag(sw, idx * 2048, lane);
+      a1 = lds_frag(sw, idx * 2048 + 1024, lane);
+    }
+    const bool mean_step = HM && s == G::KS;
+    const f16x8 yv = mean_step ? yh[G::KS] : yh[s < G::KS ? s : 0];
+    acc = mfma_h(a0, yv, acc);
+    acc = mfma_h(a1, yv, acc);
+    if (Y2 && !mean_step) acc = mfma_h(a0, yl[s < G::KS ? s : 0], acc);
+    if (s == SPS - 1) {
+      const float ps = p * sk[G::NSL + r];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) out[r][q] = fmaf(out[r][q], alpha, ps * acc[q]);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+    }
+  }
+}
+
+// The per-component scalars (slice scales, c_k) are fetched with scalar loads and waited for right
+// away, before the LDS reads of a phase: an outstanding SMEM load would force every later LDS wait
+// to lgkmcnt(0) (scalar loads return out of order), which serialises the fragment prefetch.
+template <int NS>
+struct CompScalars {
+  float s[NS];
+  double c;
+  QCE_DEV void load(const float* __restrict__ sinv, const double* __restrict__ cconst, int k) {
+    const float* sk = sinv + (long long)k * NS;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) s[i] = sk[i];
+    c = cconst[k];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+};
+
+// ---- exact-path phases with hand-counted LDS reads ---------------------------------------------
+// The fragment reads are inline-asm ds_read_b128 issued two k-steps ahead of their MFMAs and waited
+// for with a counted lgkmcnt that names the consumed registers as read-write ("+v", so no consumer
+// is scheduled above the wait, §5.7 form (ii)).  The compiler-scheduled version sank the prefetch
+// next to its use in some phases (lgkmcnt(0) before every MFMA pair).  Per-component scalars are
+// already in registers (CompScalars), so no SMEM load is in flight to disorder lgkmcnt.
+template <int OFF>
+QCE_DEV void ds_rd(f16x8& v, unsigned addr) {
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
+}
+template <int N_>
+QCE_DEV void wait_lgkm(f16x8& a, f16x8& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N_));
+}
+template <typename F, int... I>
+QCE_DEV void static_for(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+constexpr int c_gl_slice(int idx, int hmi) {
+  int r = 0, base = 0;
+  while (idx >= base + 2 * r + 2 + hmi) {
+    base += 2 * r + 2 + hmi;
+    ++r;
+  }
+  return r;
+}
+
+template <int MP, int NP, bool HM>
+QCE_DEV double gl_phase_x(const char* sl, const f16x8* yh, const float* sk, int lane) {
+  using G = H2Geom<MP, NP, HM>;
+  constexpr int NST = G::GL_STEPS;
+  const unsigned addr = (unsigned)(uintptr_t)(sl) + lane * 16;
+  f16x8 buf[NST][2];
+  ds_rd<0>(buf[0][0], addr);
+  ds_rd<1024>(buf[0][1], addr);
+  if constexpr (NST > 1) {
+    ds_rd<2048>(buf[1][0], addr);
+    ds_rd<3072>(buf[1][1], addr);
+  }
+  double quad = 0.0;
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+  static_for(
+      [&](auto ic) {
+        constexpr int idx = decltype(ic)::value;
+        constexpr int r = c_gl_slice(idx, G::HMI);
+        constexpr int s = idx - (r * (r + 1) + G::HMI * r);
+        if constexpr (idx + 2 < NST) {
+          ds_rd<(idx + 2) * 2048>(buf[idx + 2][0], addr);
+          ds_rd<(idx + 2) * 2048 + 1024>(buf[idx + 2][1], addr);
+        }
+        constexpr int pend = 2 * ((idx + 2 < NST ? idx + 2 : NST - 1) - idx);
+        wait_lgkm<pend>(buf[idx][0], buf[idx][1]);
+        constexpr bool mean_step = HM && s == 2 * r + 2;
+        const f16x8 yv = mean_step ? yh[G::KS] : yh[s < G::KS ? s : 0];
+        acc = mfma_h(buf[idx][0], yv, acc);
+        acc = mfma_h(buf[idx][1], yv, acc);
+        if constexpr (s == 2 * r + 1 + G::HMI) {  // slice complete
+          float qs = 0.0f;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) qs = fmaf(acc[q], acc[q], qs);
+          const double is = (double)sk[r];
+          quad = fma((double)qs, is * is, quad);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+        }
+      },
+      std::make_integer_sequence<int, NST>{});
+  return quad;
+}
+
+template <int MP, int NP, bool HM, int R0, int R1>
+QCE_DEV void gw_phase_x(const char* sw, const f16x8* yh, const float* sk, float p, float alpha, f32x16* out,
+                        int lane) {
+  using G = H2Geom<MP, NP, HM>;
+  constexpr int SPS = G::KS + G::HMI;
+  constexpr int NST = (R1 - R0) * SPS;
+  const unsigned addr = (unsigned)(uintptr_t)(sw) + lane * 16;
+  f16x8 buf[NST][2];
+  ds_rd<0>(buf[0][0], addr);
+  ds_rd<1024>(buf[0][1], addr);
+  if constexpr (NST > 1) {
+    ds_rd<2048>(buf[1][0], addr);
+    ds_rd<3072>(buf[1][1], addr);
+  }
+  f32x16 acc;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+  static_for(
+      [&](auto ic) {
+        constexpr int idx = decltype(ic)::value;
+        constexpr int r = R0 + idx / SPS, s = idx % SPS;
+        if constexpr (idx + 2 < NST) {
+          ds_rd<(idx + 2) * 2048>(buf[idx + 2][0], addr);
+          ds_rd<(idx + 2) * 2048 + 1024>(buf[idx + 2][1], addr);
+        }
+        constexpr int pend = 2 * ((idx + 2 < NST ? idx + 2 : NST - 1) - idx);
+        wait_lgkm<pend>(buf[idx][0], buf[idx][1]);
+        constexpr bool mean_step = HM && s == G::KS;
+        const f16x8 yv = mean_step ? yh[G::KS] : yh[s < G::KS ? s : 0];
+        acc = mfma_h(buf[idx][0], yv, acc);
+        acc = mfma_h(buf[idx][1], yv, acc);
+        if constexpr (s == SPS - 1) {
+          const float ps = p * sk[G::NSL + r];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) out[r][q] = fmaf(out[r][q], alpha, ps * acc[q]);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+        }
+      },
+      std::make_integer_sequence<int, NST>{});
+}
+
+QCE_DEV void softmax_step(double lp, double& m, double& ssum, float& alpha, float& p) {
+  const double mnew = fmax(m, lp);
+  alpha = (m == mnew) ? 1.0f : expf((float)(m - mnew));
+  p = (lp == QCE_NEG_INF) ? 0.0f : expf((float)(lp - mnew));
+  ssum = ssum * (double)alpha + (double)p;
+  m = mnew;
+}
+
+// Two-slot pipeline (any geometry): GL (slot L) and GW (slot W) of a component; GW_k streams in
+// during the GL phase, GL_{k+1} during the GW phase.
 template <int MP, int NP, bool HM, bool Y2>
 QCE_DEV void h2_kloop(int k0, int k1, const char* __restrict__ pack, long long cstride, const float* __restrict__ sinv,
                       const double* __restrict__ cconst, const f16x8* yh, const f16x8* yl, char* lds,
@@ -69,160 +370,123 @@ QCE_DEV void h2_kloop(int k0, int k1, const char* __restrict__ pack, long long c
   using G = H2Geom<MP, NP, HM>;
   char* slotL = lds;
   char* slotW = lds + G::GL_BYTES;
-  const int NSLICE = G::NSL + G::NSW;
-  // prologue: both halves of component k0
   stage<G::GL_BYTES>(pack + (long long)k0 * cstride, slotL, wave, lane);
   stage<G::GW_BYTES>(pack + (long long)k0 * cstride + G::GL_BYTES, slotW, wave, lane);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  wait_vm<0>();
+  raw_barrier();
+  CompScalars<G::NSL + G::NSW> cs;
+  cs.load(sinv, cconst, k0);
   for (int k = k0; k < k1; ++k) {
-    const float* sk = sinv + (long long)k * NSLICE;
-    // ---- GL phase: whitened residual u = E(Linv)[y;1], quad form in FP64 ----
-    double quad = 0.0;
-#pragma unroll
-    for (int r = 0; r < G::NSL; ++r) {
-      f32x16 acc;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
-      const int base = G::gl_off(r) * 2048;
-#pragma unroll
-      for (int s = 0; s < 2 * r + 2; ++s) {
-        const f16x8 a0 = lds_frag(slotL, base + s * 2048, lane);
-        const f16x8 a1 = lds_frag(slotL, base + s * 2048 + 1024, lane);
-        acc = mfma_h(a0, yh[s], acc);
-        acc = mfma_h(a1, yh[s], acc);
-        if (Y2) acc = mfma_h(a0, yl[s], acc);
-      }
-      if (HM) {
-        const f16x8 a0 = lds_frag(slotL, base + (2 * r + 2) * 2048, lane);
-        const f16x8 a1 = lds_frag(slotL, base + (2 * r + 2) * 2048 + 1024, lane);
-        acc = mfma_h(a0, yh[G::KS], acc);
-        acc = mfma_h(a1, yh[G::KS], acc);
-      }
-      float qs = 0.0f;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) qs = fmaf(acc[q], acc[q], qs);
-      const double is = (double)sk[r];
-      quad = fma((double)qs, is * is, quad);
-    }
+    const float* sk = cs.s;
+    double quad = gl_phase<MP, NP, HM, Y2>(slotL, yh, yl, sk, lane);
     quad += __shfl_xor(quad, 32);
-    const double lp = cconst[k] - quad;
-    const double mnew = fmax(m, lp);
-    const float alpha = (m == mnew) ? 1.0f : expf((float)(m - mnew));
-    const float p = (lp == QCE_NEG_INF) ? 0.0f : expf((float)(lp - mnew));
-    ssum = ssum * (double)alpha + (double)p;
-    m = mnew;
-    // GW_k has to have landed before its phase; slotL is free once every wave passed here
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    float alpha, p;
+    softmax_step(cs.c - quad, m, ssum, alpha, p);
+    wait_vm<0>();  // GW_k landed
+    raw_barrier();  // and every wave is done with slot L
     if (k + 1 < k1) stage<G::GL_BYTES>(pack + (long long)(k + 1) * cstride, slotL, wave, lane);
-    // ---- GW phase: Z = E(W)[y;1], folded into the running accumulator ----
-#pragma unroll
-    for (int r = 0; r < G::NSW; ++r) {
-      f32x16 acc;
-#pragma unroll
-      for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
-      const int base = r * (G::KS + G::HMI) * 2048;
-#pragma unroll
-      for (int s = 0; s < G::KS; ++s) {
-        const f16x8 a0 = lds_frag(slotW, base + s * 2048, lane);
-        const f16x8 a1 = lds_frag(slotW, base + s * 2048 + 1024, lane);
-        acc = mfma_h(a0, yh[s], acc);
-        acc = mfma_h(a1, yh[s], acc);
-        if (Y2) acc = mfma_h(a0, yl[s], acc);
-      }
-      if (HM) {
-        const f16x8 a0 = lds_frag(slotW, base + G::KS * 2048, lane);
-        const f16x8 a1 = lds_frag(slotW, base + G::KS * 2048 + 1024, lane);
-        acc = mfma_h(a0, yh[G::KS], acc);
-        acc = mfma_h(a1, yh[G::KS], acc);
-      }
-      const float ps = p * sk[G::NSL + r];
-#pragma unroll
-      for (int q = 0; q < 16; ++q) out[r][q] = fmaf(out[r][q], alpha, ps * acc[q]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    gw_phase<MP, NP, HM, Y2, 0, G::NSW>(slotW, yh, yl, sk, p, alpha, out, lane);
+    if (k + 1 < k1) cs.load(sinv, cconst, k + 1);
+    wait_vm<0>();
+    raw_barrier();
     if (k + 1 < k1) stage<G::GW_BYTES>(pack + (long long)(k + 1) * cstride + G::GL_BYTES, slotW, wave, lane);
   }
 }
 
-// PARTIAL: write (m, s, acc) for split blockIdx.y (row = split * B + sample); else the final h.
-template <int MP, int NP, bool HM, bool PARTIAL>
-__global__ __launch_bounds__(512) void k_est_all_h2(long long B, int M, int N, int K, int nsplit, double y_scale,
-                                                    const double2* __restrict__ y, const char* __restrict__ pack,
-                                                    long long cstride, const float* __restrict__ sinv,
-                                                    const double* __restrict__ cconst, double2* __restrict__ h,
-                                                    double* __restrict__ part_m, double* __restrict__ part_s,
-                                                    float* __restrict__ part_acc) {
-  using G = H2Geom<MP, NP, HM>;
-  __shared__ __attribute__((aligned(16))) char lds[G::COMP_BYTES];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int j = lane & 31, hh = lane >> 5;
-  const long long sample = (long long)blockIdx.x * 256 + wave * 32 + j;
-  const bool valid = sample < B;
-  // split-K range
-  const int split = blockIdx.y;
-  const int kb = (int)(((long long)K * split) / nsplit), ke = (int)(((long long)K * (split + 1)) / nsplit);
-
-  // Y^T fragments: k-step s covers real features 16s + 8hh + t (t = 0..7) = complex 8s + 4hh + t/2
-  f16x8 yh[G::KS + G::HMI], yl[G::KS];
-  bool inexact = false;
-#pragma unroll
-  for (int s = 0; s < G::KS; ++s) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int c = 8 * s + 4 * hh + t;
-      double2 v = make_double2(0.0, 0.0);
-      if (valid && c < M) v = y[sample * M + c];
-      const double re = v.x * y_scale, im = v.y * y_scale;
-      const _Float16 rh = (_Float16)re, ih = (_Float16)im;
-      const _Float16 rl = (_Float16)(re - (double)rh), il = (_Float16)(im - (double)ih);
-      yh[s][2 * t] = rh;
-      yh[s][2 * t + 1] = ih;
-      yl[s][2 * t] = rl;
-      yl[s][2 * t + 1] = il;
-      inexact |= (rl != (_Float16)0.0f) || (il != (_Float16)0.0f);
+// Deep pipeline for MP = NP = 64 without means (the benchmark shape): each component is three
+// chunks — GL (40 KB), GW slices 0-1 (32 KB), GW slices 2-3 (32 KB) — streamed through a ring of
+// four 40 KB LDS slots, chunk c in slot c % 4; the barrier that ends phase c refills that slot with
+// chunk c + 4, so every chunk has three compute phases to land.  Waits are counted: vmcnt(N) keeps
+// the two younger chunks in flight (5 global_load_lds per wave for GL, 4 for a GW half).
+template <bool Y2>
+QCE_DEV void h2_kloop_deep(int k0, int k1, const char* __restrict__ pack, long long cstride,
+                           const float* __restrict__ sinv, const double* __restrict__ cconst, const f16x8* yh,
+                           const f16x8* yl, char* lds, f32x16 (&out)[4], double& m, double& ssum, int wave,
+                           int lane) {
+  using G = H2Geom<64, 64, false>;
+  constexpr int SLOT = 40960, GLB = G::GL_BYTES, GWH = G::GW_BYTES / 2;
+  static_assert(GLB == 40960 && GWH == 32768, "deep pipeline geometry");
+  const int nchunks = 3 * (k1 - k0);
+  auto issue = [&](int c) {
+    const int k = k0 + c / 3, t = c % 3;
+    const char* src = pack + (long long)k * cstride + (t == 0 ? 0 : GLB + (t - 1) * GWH);
+    char* dst = lds + (c & 3) * SLOT;
+    if (t == 0)
+      stage<GLB>(src, dst, wave, lane);
+    else
+      stage<GWH>(src, dst, wave, lane);
+  };
+  auto end_phase = [&](int c, int pos) {  // pos = c % 3 (0: GL, 1: GW first half, 2: GW second half)
+    if (c + 3 < nchunks) {
+      if (pos == 2) wait_vm<8>(); else wait_vm<9>();
+    } else if (c + 2 < nchunks) {
+      if (pos == 1) wait_vm<5>(); else wait_vm<4>();
+    } else {
+      wait_vm<0>();
     }
+    raw_barrier();
+    if (c + 4 < nchunks) issue(c + 4);
+  };
+  QCE_STAMP_DECL
+  for (int c = 0; c < 4 && c < nchunks; ++c) issue(c);
+  CompScalars<G::NSL + G::NSW> cs;
+  cs.load(sinv, cconst, k0);
+  if (nchunks >= 4) wait_vm<13>(); else wait_vm<0>();
+  raw_barrier();
+  QCE_STAMP(-1);
+  for (int k = k0; k < k1; ++k) {
+    const int c = 3 * (k - k0);
+    const float* sk = cs.s;
+    double quad = Y2 ? gl_phase<64, 64, false, Y2>(lds + (c & 3) * SLOT, yh, yl, sk, lane)
+                     : gl_phase_x<64, 64, false>(lds + (c & 3) * SLOT, yh, sk, lane);
+    QCE_STAMP(0);
+    quad += __shfl_xor(quad, 32);
+    float alpha, p;
+    softmax_step(cs.c - quad, m, ssum, alpha, p);
+    QCE_STAMP(1);
+    end_phase(c, 0);
+    QCE_STAMP(2);
+    if (Y2)
+      gw_phase<64, 64, false, Y2, 0, 2>(lds + ((c + 1) & 3) * SLOT, yh, yl, sk, p, alpha, out, lane);
+    else
+      gw_phase_x<64, 64, false, 0, 2>(lds + ((c + 1) & 3) * SLOT, yh, sk, p, alpha, out, lane);
+    QCE_STAMP(3);
+    end_phase(c + 1, 1);
+    QCE_STAMP(4);
+    if (Y2)
+      gw_phase<64, 64, false, Y2, 2, 4>(lds + ((c + 2) & 3) * SLOT, yh, yl, sk, p, alpha, out, lane);
+    else
+      gw_phase_x<64, 64, false, 2, 4>(lds + ((c + 2) & 3) * SLOT, yh, sk, p, alpha, out, lane);
+    QCE_STAMP(5);
+    if (k + 1 < k1) cs.load(sinv, cconst, k + 1);
+    end_phase(c + 2, 2);
+    QCE_STAMP(6);
   }
-  if (HM) {
-#pragma unroll
-    for (int t = 0; t < 8; ++t) yh[G::KS][t] = (_Float16)0.0f;
-    if (hh == 0) yh[G::KS][0] = (_Float16)1.0f;  // the [y; 1] augmentation column
-  }
-  f32x16 out[G::NSW];
-#pragma unroll
-  for (int r = 0; r < G::NSW; ++r)
-#pragma unroll
-    for (int q = 0; q < 16; ++q) out[r][q] = 0.0f;
-  double m = QCE_NEG_INF, ssum = 0.0;
-  if (__ballot(inexact) != 0ull)
-    h2_kloop<MP, NP, HM, true>(kb, ke, pack, cstride, sinv, cconst, yh, yl, lds, out, m, ssum, wave, lane);
-  else
-    h2_kloop<MP, NP, HM, false>(kb, ke, pack, cstride, sinv, cconst, yh, yl, lds, out, m, ssum, wave, lane);
+  QCE_STAMP_FLUSH
+}
 
-  if (!valid) return;
-  if (PARTIAL) {
-    const long long row = (long long)split * B + sample;
+QCE_DEV void write_final(double2* __restrict__ h, double* __restrict__ om, double* __restrict__ os,
+                         float* __restrict__ oa, long long row, int N, int hh, int NSW, const f32x16* out, double m,
+                         double ssum, bool partial_fmt) {
+  if (partial_fmt) {
     if (hh == 0) {
-      part_m[row] = m;
-      part_s[row] = ssum;
+      om[row] = m;
+      os[row] = ssum;
     }
-    float* pa = part_acc + row * (2LL * N);
-#pragma unroll
-    for (int r = 0; r < G::NSW; ++r)
+    float* pa = oa + row * (2LL * N);
+    for (int r = 0; r < NSW; ++r)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n0 = 16 * r + 4 * q + 2 * hh;
         if (n0 < N) *reinterpret_cast<float2*>(pa + 2 * n0) = make_float2(out[r][4 * q + 0], out[r][4 * q + 1]);
-        if (n0 + 1 < N) *reinterpret_cast<float2*>(pa + 2 * n0 + 2) = make_float2(out[r][4 * q + 2], out[r][4 * q + 3]);
+        if (n0 + 1 < N)
+          *reinterpret_cast<float2*>(pa + 2 * n0 + 2) = make_float2(out[r][4 * q + 2], out[r][4 * q + 3]);
       }
     return;
   }
   const double inv = 1.0 / ssum;
-  double2* hp = h + sample * N;
-#pragma unroll
-  for (int r = 0; r < G::NSW; ++r)
+  double2* hp = h + row * N;
+  for (int r = 0; r < NSW; ++r)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int n0 = 16 * r + 4 * q + 2 * hh;
@@ -231,28 +495,408 @@ __global__ __launch_bounds__(512) void k_est_all_h2(long long B, int M, int N, i
     }
 }
 
-// Merge nsplit partials per sample: h = sum_j acc_j e^{m_j - M} / sum_j s_j e^{m_j - M}
-// (final) or the merged partial (m, s, acc) for a further cross-GPU combine.
-__global__ __launch_bounds__(256) void k_merge_splits(long long B, int N, int nsplit, const double* __restrict__ pm,
-                                                      const double* __restrict__ ps, const float* __restrict__ pa,
-                                                      double2* __restrict__ h, double* __restrict__ om,
-                                                      double* __restrict__ os, float* __restrict__ oa) {
+// Persistent data-parallel + stream-K kernel, one instance per observation class:
+// EXACT = observations exact in fp16 after the y scale (two products per MAC, no y_lo registers),
+// !EXACT = the general three-product path.  k_y_exact sets *yflag when some observation is not
+// exact; the instance that does not match returns at once, so the choice needs no host round trip.
+// P = gridDim.x workgroups.  First R = floor(tiles/P) rounds of whole tiles (tile r*P + w,
+// components 0..K-1 in order: every workgroup streams the same component at the same time, so each
+// XCD's L2 serves it to all its CUs); then the remaining tiles' (tile, component) items are dealt
+// out L consecutive items per workgroup (stream-K).  Complete tiles are written directly — final h,
+// or the (m, s, acc) partial format when OUT_PARTIAL (K-shard path); a tail tile cut between
+// workgroups leaves its pieces in scratch record (2w + slot) * 256 + sample (slot 0: the
+// workgroup's first tail tile, 1: its last), combined by k_merge_streamk.
+template <int MP, int NP, bool HM, bool OUT_PARTIAL, bool EXACT>
+__global__ __launch_bounds__(512) void k_est_all_h2(long long B, int M, int N, int K, int R, long long L,
+                                                    double y_scale, const int* __restrict__ yflag,
+                                                    const double2* __restrict__ y, const char* __restrict__ pack,
+                                                    long long cstride, const float* __restrict__ sinv,
+                                                    const double* __restrict__ cconst, double2* __restrict__ h,
+                                                    double* __restrict__ om, double* __restrict__ os,
+                                                    float* __restrict__ oa, double* __restrict__ pm,
+                                                    double* __restrict__ ps, float* __restrict__ pa) {
+  using G = H2Geom<MP, NP, HM>;
+  constexpr bool DEEP = EXACT && MP == 64 && NP == 64 && !HM;
+  __shared__ __attribute__((aligned(16))) char lds[DEEP ? 4 * 40960 : G::COMP_BYTES];
+  if (EXACT == (*yflag != 0)) return;  // the other instance handles this batch
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = lane & 31, hh = lane >> 5;
+  const long long P = gridDim.x, w = blockIdx.x;
+  const long long tiles = (B + 255) / 256;
+  const long long tail0 = (long long)R * P;  // first tail tile
+  const long long item0 = w * L;
+  const long long item1 = (item0 + L < (tiles - tail0) * K) ? item0 + L : (tiles - tail0) * K;
+  const long long t_first = tail0 + (L > 0 ? item0 / K : 0);
+  const long long nseg = (long long)R + (item1 > item0 ? (item1 - 1) / K - item0 / K + 1 : 0);
+  for (long long seg = 0; seg < nseg; ++seg) {
+    long long t;
+    int klo, khi;
+    if (seg < R) {
+      t = seg * P + w;
+      klo = 0;
+      khi = K;
+    } else {
+      t = tail0 + item0 / K + (seg - R);
+      const long long tK = (t - tail0) * K;
+      klo = (int)((item0 > tK ? item0 : tK) - tK);
+      khi = (int)((tK + K < item1 ? tK + K : item1) - tK);
+    }
+    const int ls = wave * 32 + j;
+    const long long sample = t * 256 + ls;
+    const bool valid = sample < B;
+    // Y^T fragments: k-step s covers real features 16s + 8hh + e (e = 0..7) = complex 8s + 4hh + e/2
+    f16x8 yh[G::KS + G::HMI], yl[EXACT ? 1 : G::KS];
+#pragma unroll
+    for (int s = 0; s < G::KS; ++s) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = 8 * s + 4 * hh + e;
+        double2 v = make_double2(0.0, 0.0);
+        if (valid && c < M) v = y[sample * M + c];
+        const double re = v.x * y_scale, im = v.y * y_scale;
+        const _Float16 rh = (_Float16)re, ih = (_Float16)im;
+        yh[s][2 * e] = rh;
+        yh[s][2 * e + 1] = ih;
+        if (!EXACT) {
+          yl[s][2 * e] = (_Float16)(re - (double)rh);
+          yl[s][2 * e + 1] = (_Float16)(im - (double)ih);
+        }
+      }
+    }
+    if (HM) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) yh[G::KS][e] = (_Float16)0.0f;
+      if (hh == 0) yh[G::KS][0] = (_Float16)1.0f;  // the [y; 1] augmentation column
+    }
+    f32x16 out[G::NSW];
+#pragma unroll
+    for (int r = 0; r < G::NSW; ++r)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) out[r][q] = 0.0f;
+    double m = QCE_NEG_INF, ssum = 0.0;
+    if constexpr (DEEP)
+      h2_kloop_deep<false>(klo, khi, pack, cstride, sinv, cconst, yh, yl, lds, out, m, ssum, wave, lane);
+    else
+      h2_kloop<MP, NP, HM, !EXACT>(klo, khi, pack, cstride, sinv, cconst, yh, yl, lds, out, m, ssum, wave, lane);
+    if (!valid) continue;
+    if (klo == 0 && khi == K) {
+      write_final(h, om, os, oa, sample, N, hh, G::NSW, out, m, ssum, OUT_PARTIAL);
+    } else {
+      const long long rec = (w * 2 + (t == t_first ? 0 : 1)) * 256 + ls;
+      write_final(nullptr, pm, ps, pa, rec, N, hh, G::NSW, out, m, ssum, true);
+    }
+  }
+}
+
+// ================================================================================================
+// Wide variant for the benchmark geometry (MP = NP = 64, zero means, exact observations):
+// one wave per SIMD (4 waves, 256 threads, up to 512 registers per lane), each wave owning 64
+// samples as two 32-column MFMA tiles.  Every LDS fragment then feeds two independent MFMA chains
+// (half the LDS reads per MFMA of the 8-wave version), and one wave's epilogue VALU can run beside
+// its other tile's MFMAs.  Same 3-chunk / 4-slot LDS ring, staged by 4 waves (GL chunk: 10
+// global_load_lds per wave, GW half: 8).
+// ================================================================================================
+template <int BYTES>
+QCE_DEV void stage4(const char* __restrict__ src, char* dst, int wave, int lane) {
+  wave = __builtin_amdgcn_readfirstlane(wave);
+#pragma unroll
+  for (int c = wave; c < BYTES / 1024; c += 4) {
+    __builtin_amdgcn_global_load_lds((const void*)(src + c * 1024 + lane * 16),
+                                     (__attribute__((address_space(3))) void*)(dst + c * 1024), 16, 0, 0);
+  }
+}
+
+template <int N_>
+QCE_DEV void wait_vm_w() {
+  if constexpr (N_ == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if constexpr (N_ == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+  else if constexpr (N_ == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  else if constexpr (N_ == 18) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+  else if constexpr (N_ == 26) asm volatile("s_waitcnt vmcnt(26)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// full cross-half sum of a per-lane double (lanes l and l+32 hold the two halves of a column)
+QCE_DEV double sum_halves(double q, int lane) {
+  const unsigned lo = __double2loint(q), hi = __double2hiint(q);
+  const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+  const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+  const bool low = lane < 32;
+  const double other = __hiloint2double(low ? b[1] : b[0], low ? a[1] : a[0]);
+  return q + other;
+}
+
+QCE_DEV double gl_phase_w(const char* sl, const f16x8 (&yh)[2][8], const float* sk, int lane, double& quad1) {
+  using G = H2Geom<64, 64, false>;
+  constexpr int NST = G::GL_STEPS;  // 20
+  const unsigned addr = (unsigned)(uintptr_t)(sl) + lane * 16;
+  f16x8 buf[NST][2];
+  ds_rd<0>(buf[0][0], addr);
+  ds_rd<1024>(buf[0][1], addr);
+  ds_rd<2048>(buf[1][0], addr);
+  ds_rd<3072>(buf[1][1], addr);
+  double q0 = 0.0, q1 = 0.0;
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    acc0[q] = 0.0f;
+    acc1[q] = 0.0f;
+  }
+  static_for(
+      [&](auto ic) {
+        constexpr int idx = decltype(ic)::value;
+        constexpr int r = c_gl_slice(idx, 0);
+        constexpr int s = idx - r * (r + 1);
+        if constexpr (idx + 2 < NST) {
+          ds_rd<(idx + 2) * 2048>(buf[idx + 2][0], addr);
+          ds_rd<(idx + 2) * 2048 + 1024>(buf[idx + 2][1], addr);
+        }
+        constexpr int pend = 2 * ((idx + 2 < NST ? idx + 2 : NST - 1) - idx);
+        wait_lgkm<pend>(buf[idx][0], buf[idx][1]);
+        acc0 = mfma_h(buf[idx][0], yh[0][s], acc0);
+        acc1 = mfma_h(buf[idx][0], yh[1][s], acc1);
+        acc0 = mfma_h(buf[idx][1], yh[0][s], acc0);
+        acc1 = mfma_h(buf[idx][1], yh[1][s], acc1);
+        if constexpr (s == 2 * r + 1) {
+          float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            s0 = fmaf(acc0[q], acc0[q], s0);
+            s1 = fmaf(acc1[q], acc1[q], s1);
+          }
+          const double is = (double)sk[r];
+          q0 = fma((double)s0, is * is, q0);
+          q1 = fma((double)s1, is * is, q1);
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            acc0[q] = 0.0f;
+            acc1[q] = 0.0f;
+          }
+        }
+      },
+      std::make_integer_sequence<int, NST>{});
+  quad1 = q1;
+  return q0;
+}
+
+template <int R0, int R1>
+QCE_DEV void gw_phase_w(const char* sw, const f16x8 (&yh)[2][8], const float* sk, const float (&p)[2],
+                        const float (&alpha)[2], f32x16 (&out)[2][4], int lane) {
+  using G = H2Geom<64, 64, false>;
+  constexpr int SPS = G::KS;
+  constexpr int NST = (R1 - R0) * SPS;
+  const unsigned addr = (unsigned)(uintptr_t)(sw) + lane * 16;
+  f16x8 buf[NST][2];
+  ds_rd<0>(buf[0][0], addr);
+  ds_rd<1024>(buf[0][1], addr);
+  ds_rd<2048>(buf[1][0], addr);
+  ds_rd<3072>(buf[1][1], addr);
+  f32x16 acc0, acc1;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    acc0[q] = 0.0f;
+    acc1[q] = 0.0f;
+  }
+  static_for(
+      [&](auto ic) {
+        constexpr int idx = decltype(ic)::value;
+        constexpr int r = R0 + idx / SPS, s = idx % SPS;
+        if constexpr (idx + 2 < NST) {
+          ds_rd<(idx + 2) * 2048>(buf[idx + 2][0], addr);
+          ds_rd<(idx + 2) * 2048 + 1024>(buf[idx + 2][1], addr);
+        }
+        constexpr int pend = 2 * ((idx + 2 < NST ? idx + 2 : NST - 1) - idx);
+        wait_lgkm<pend>(buf[idx][0], buf[idx][1]);
+        acc0 = mfma_h(buf[idx][0], yh[0][s], acc0);
+        acc1 = mfma_h(buf[idx][0], yh[1][s], acc1);
+        acc0 = mfma_h(buf[idx][1], yh[0][s], acc0);
+        acc1 = mfma_h(buf[idx][1], yh[1][s], acc1);
+        if constexpr (s == SPS - 1) {
+          const float sc = sk[G::NSL + r];
+          const float ps0 = p[0] * sc, ps1 = p[1] * sc;
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            out[0][r][q] = fmaf(out[0][r][q], alpha[0], ps0 * acc0[q]);
+            out[1][r][q] = fmaf(out[1][r][q], alpha[1], ps1 * acc1[q]);
+          }
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            acc0[q] = 0.0f;
+            acc1[q] = 0.0f;
+          }
+        }
+      },
+      std::make_integer_sequence<int, NST>{});
+}
+
+QCE_DEV void h2w_kloop(int k0, int k1, const char* __restrict__ pack, long long cstride,
+                       const float* __restrict__ sinv, const double* __restrict__ cconst, const f16x8 (&yh)[2][8],
+                       char* lds, f32x16 (&out)[2][4], double (&m)[2], double (&ssum)[2], int wave, int lane) {
+  using G = H2Geom<64, 64, false>;
+  constexpr int SLOT = 40960, GLB = G::GL_BYTES, GWH = G::GW_BYTES / 2;
+  const int nchunks = 3 * (k1 - k0);
+  auto issue = [&](int c) {
+    const int k = k0 + c / 3, t = c % 3;
+    const char* src = pack + (long long)k * cstride + (t == 0 ? 0 : GLB + (t - 1) * GWH);
+    char* dst = lds + (c & 3) * SLOT;
+    if (t == 0)
+      stage4<GLB>(src, dst, wave, lane);
+    else
+      stage4<GWH>(src, dst, wave, lane);
+  };
+  // ops per wave: GL chunk 10, GW half 8; keep the two younger chunks in flight
+  auto end_phase = [&](int c, int pos) {
+    if (c + 3 < nchunks) {
+      if (pos == 2) wait_vm_w<16>(); else wait_vm_w<18>();
+    } else if (c + 2 < nchunks) {
+      if (pos == 1) wait_vm_w<10>(); else wait_vm_w<8>();
+    } else {
+      wait_vm_w<0>();
+    }
+    raw_barrier();
+    if (c + 4 < nchunks) issue(c + 4);
+  };
+  for (int c = 0; c < 4 && c < nchunks; ++c) issue(c);
+  CompScalars<G::NSL + G::NSW> cs;
+  cs.load(sinv, cconst, k0);
+  if (nchunks >= 4) wait_vm_w<26>(); else wait_vm_w<0>();
+  raw_barrier();
+  for (int k = k0; k < k1; ++k) {
+    const int c = 3 * (k - k0);
+    double q1;
+    double q0 = gl_phase_w(lds + (c & 3) * SLOT, yh, cs.s, lane, q1);
+    q0 = sum_halves(q0, lane);
+    q1 = sum_halves(q1, lane);
+    float alpha[2], p[2];
+    softmax_step(cs.c - q0, m[0], ssum[0], alpha[0], p[0]);
+    softmax_step(cs.c - q1, m[1], ssum[1], alpha[1], p[1]);
+    end_phase(c, 0);
+    gw_phase_w<0, 2>(lds + ((c + 1) & 3) * SLOT, yh, cs.s, p, alpha, out, lane);
+    end_phase(c + 1, 1);
+    gw_phase_w<2, 4>(lds + ((c + 2) & 3) * SLOT, yh, cs.s, p, alpha, out, lane);
+    if (k + 1 < k1) cs.load(sinv, cconst, k + 1);
+    end_phase(c + 2, 2);
+  }
+}
+
+template <bool OUT_PARTIAL>
+__global__ __launch_bounds__(256) void k_est_all_h2w(long long B, int M, int N, int K, int R, long long L,
+                                                     double y_scale, const int* __restrict__ yflag,
+                                                     const double2* __restrict__ y, const char* __restrict__ pack,
+                                                     long long cstride, const float* __restrict__ sinv,
+                                                     const double* __restrict__ cconst, double2* __restrict__ h,
+                                                     double* __restrict__ om, double* __restrict__ os,
+                                                     float* __restrict__ oa, double* __restrict__ pm,
+                                                     double* __restrict__ ps, float* __restrict__ pa) {
+  using G = H2Geom<64, 64, false>;
+  __shared__ __attribute__((aligned(16))) char lds[4 * 40960];
+  if (*yflag != 0) return;  // inexact observations: the general 8-wave instance runs instead
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j = lane & 31, hh = lane >> 5;
+  const long long P = gridDim.x, w = blockIdx.x;
+  const long long tiles = (B + 255) / 256;
+  const long long tail0 = (long long)R * P;
+  const long long item0 = w * L;
+  const long long item1 = (item0 + L < (tiles - tail0) * K) ? item0 + L : (tiles - tail0) * K;
+  const long long t_first = tail0 + (L > 0 ? item0 / K : 0);
+  const long long nseg = (long long)R + (item1 > item0 ? (item1 - 1) / K - item0 / K + 1 : 0);
+  for (long long seg = 0; seg < nseg; ++seg) {
+    long long t;
+    int klo, khi;
+    if (seg < R) {
+      t = seg * P + w;
+      klo = 0;
+      khi = K;
+    } else {
+      t = tail0 + item0 / K + (seg - R);
+      const long long tK = (t - tail0) * K;
+      klo = (int)((item0 > tK ? item0 : tK) - tK);
+      khi = (int)((tK + K < item1 ? tK + K : item1) - tK);
+    }
+    f16x8 yh[2][8];
+#pragma unroll
+    for (int tw = 0; tw < 2; ++tw) {
+      const long long sample = t * 256 + wave * 64 + tw * 32 + j;
+      const bool valid = sample < B;
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = 8 * s + 4 * hh + e;
+          double2 v = make_double2(0.0, 0.0);
+          if (valid && c < M) v = y[sample * M + c];
+          yh[tw][s][2 * e] = (_Float16)(v.x * y_scale);
+          yh[tw][s][2 * e + 1] = (_Float16)(v.y * y_scale);
+        }
+    }
+    f32x16 out[2][4];
+#pragma unroll
+    for (int tw = 0; tw < 2; ++tw)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) out[tw][r][q] = 0.0f;
+    double m[2] = {QCE_NEG_INF, QCE_NEG_INF}, ssum[2] = {0.0, 0.0};
+    h2w_kloop(klo, khi, pack, cstride, sinv, cconst, yh, lds, out, m, ssum, wave, lane);
+#pragma unroll
+    for (int tw = 0; tw < 2; ++tw) {
+      const int ls = wave * 64 + tw * 32 + j;
+      const long long sample = t * 256 + ls;
+      if (sample >= B) continue;
+      if (klo == 0 && khi == K) {
+        write_final(h, om, os, oa, sample, N, hh, G::NSW, out[tw], m[tw], ssum[tw], OUT_PARTIAL);
+      } else {
+        const long long rec = (w * 2 + (t == t_first ? 0 : 1)) * 256 + ls;
+        write_final(nullptr, pm, ps, pa, rec, N, hh, G::NSW, out[tw], m[tw], ssum[tw], true);
+      }
+    }
+  }
+}
+
+// *flag |= (some y * y_scale is not exactly representable in fp16)
+__global__ __launch_bounds__(256) void k_y_exact(long long n, const double* __restrict__ y, double y_scale,
+                                                 int* __restrict__ flag) {
+  bool bad = false;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const double v = y[i] * y_scale;
+    const _Float16 hv = (_Float16)v;
+    bad |= (_Float16)(v - (double)hv) != (_Float16)0.0f;
+  }
+  if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+// Combine the stream-K pieces of the tiles that were cut between workgroups (one wave per
+// sample; complete tiles return at once): h = sum_j acc_j e^{m_j - M} / sum_j s_j e^{m_j - M},
+// or the merged (m, s, acc) partial when h == nullptr.
+__global__ __launch_bounds__(256) void k_merge_streamk(long long B, int N, int K, long long tail0, long long L,
+                                                       const double* __restrict__ pm, const double* __restrict__ ps,
+                                                       const float* __restrict__ pa, double2* __restrict__ h,
+                                                       double* __restrict__ om, double* __restrict__ os,
+                                                       float* __restrict__ oa) {
   const long long b = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (b >= B) return;
+  const long long t = b / 256 - tail0, ls = b % 256;
+  if (t < 0 || L <= 0) return;  // data-parallel tile: complete, written by its workgroup
+  const long long wa = (t * K) / L, wb = ((t + 1) * K - 1) / L;
+  if (wa == wb) return;  // complete tile, already written by its workgroup
+  auto rec_of = [&](long long w) -> long long {
+    const long long tf = (w * L) / K;
+    return (w * 2 + (t == tf ? 0 : 1)) * 256 + ls;
+  };
   double mx = QCE_NEG_INF;
-  for (int j = 0; j < nsplit; ++j) mx = fmax(mx, pm[(long long)j * B + b]);
+  for (long long w = wa; w <= wb; ++w) mx = fmax(mx, pm[rec_of(w)]);
   double s = 0.0;
-  for (int j = 0; j < nsplit; ++j) {
-    const double mj = pm[(long long)j * B + b];
-    s += (mj == QCE_NEG_INF) ? 0.0 : ps[(long long)j * B + b] * exp(mj - mx);
+  for (long long w = wa; w <= wb; ++w) {
+    const long long r = rec_of(w);
+    s += (pm[r] == QCE_NEG_INF) ? 0.0 : ps[r] * exp(pm[r] - mx);
   }
   for (int n = lane; n < N; n += 64) {
     double re = 0.0, im = 0.0;
-    for (int j = 0; j < nsplit; ++j) {
-      const double mj = pm[(long long)j * B + b];
-      const double sc = (mj == QCE_NEG_INF) ? 0.0 : exp(mj - mx);
-      const float2 v = *reinterpret_cast<const float2*>(pa + ((long long)j * B + b) * 2 * N + 2 * n);
+    for (long long w = wa; w <= wb; ++w) {
+      const long long r = rec_of(w);
+      const double sc = (pm[r] == QCE_NEG_INF) ? 0.0 : exp(pm[r] - mx);
+      const float2 v = *reinterpret_cast<const float2*>(pa + r * 2 * N + 2 * n);
       re += (double)v.x * sc;
       im += (double)v.y * sc;
     }
@@ -359,55 +1003,86 @@ hipError_t qce_launch_pack_h2(int K, int M, int N, int MP, int NP, int has_mean,
 // ---------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------
-template <int MP, int NP, bool HM>
-static hipError_t launch_h2_t(const QceH2Args& a, double2* h, double* pm, double* ps, float* pa, bool partial,
-                              hipStream_t st) {
-  dim3 grid((unsigned)((a.B + 255) / 256), (unsigned)a.nsplit);
-  if (partial)
-    hipLaunchKernelGGL((k_est_all_h2<MP, NP, HM, true>), grid, dim3(512), 0, st, a.B, a.M, a.N, a.K, a.nsplit,
-                       a.y_scale, a.y, a.pack, a.cstride, a.sinv, a.cconst, h, pm, ps, pa);
-  else
-    hipLaunchKernelGGL((k_est_all_h2<MP, NP, HM, false>), grid, dim3(512), 0, st, a.B, a.M, a.N, a.K, a.nsplit,
-                       a.y_scale, a.y, a.pack, a.cstride, a.sinv, a.cconst, h, pm, ps, pa);
+template <int MP, int NP, bool HM, bool OP>
+static hipError_t launch_h2_pair(const QceH2Args& a, hipStream_t st) {
+  dim3 grid((unsigned)a.nwg);
+  if constexpr (MP == 64 && NP == 64 && !HM) {
+    const char* e = getenv("QCE_H2_WIDE");
+    if (e && e[0] == '1')
+      hipLaunchKernelGGL((k_est_all_h2w<OP>), grid, dim3(256), 0, st, a.B, a.M, a.N, a.K, a.R, a.L, a.y_scale,
+                         a.yflag, a.y, a.pack, a.cstride, a.sinv, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa);
+    else
+      hipLaunchKernelGGL((k_est_all_h2<MP, NP, HM, OP, true>), grid, dim3(512), 0, st, a.B, a.M, a.N, a.K, a.R,
+                         a.L, a.y_scale, a.yflag, a.y, a.pack, a.cstride, a.sinv, a.cconst, a.h, a.om, a.os, a.oa,
+                         a.pm, a.ps, a.pa);
+  } else {
+    hipLaunchKernelGGL((k_est_all_h2<MP, NP, HM, OP, true>), grid, dim3(512), 0, st, a.B, a.M, a.N, a.K, a.R, a.L,
+                       a.y_scale, a.yflag, a.y, a.pack, a.cstride, a.sinv, a.cconst, a.h, a.om, a.os, a.oa, a.pm,
+                       a.ps, a.pa);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_est_all_h2<MP, NP, HM, OP, false>), grid, dim3(512), 0, st, a.B, a.M, a.N, a.K, a.R, a.L,
+                     a.y_scale, a.yflag, a.y, a.pack, a.cstride, a.sinv, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps,
+                     a.pa);
   return hipGetLastError();
 }
 
-hipError_t qce_launch_est_h2(const QceH2Args& a, double2* h, double* pm, double* ps, float* pa, bool partial,
-                             hipStream_t st) {
+template <int MP, int NP, bool HM>
+static hipError_t launch_h2_t(const QceH2Args& a, bool out_partial, hipStream_t st) {
+  return out_partial ? launch_h2_pair<MP, NP, HM, true>(a, st) : launch_h2_pair<MP, NP, HM, false>(a, st);
+}
+
+#define QCE_H2_SHAPES(X) \
+  X(16, 16) X(16, 32) X(16, 64) X(32, 16) X(32, 32) X(32, 64) X(64, 16) X(64, 32) X(64, 64)
+
+hipError_t qce_launch_est_h2(const QceH2Args& a, bool out_partial, hipStream_t st) {
   const bool hm = a.has_mean != 0;
-#define QCE_CASE(X, Y)                                                                    \
-  if (a.MP == X && a.NP == Y)                                                             \
-    return hm ? launch_h2_t<X, Y, true>(a, h, pm, ps, pa, partial, st)                    \
-              : launch_h2_t<X, Y, false>(a, h, pm, ps, pa, partial, st);
-  QCE_CASE(16, 16)
-  QCE_CASE(16, 32)
-  QCE_CASE(16, 64)
-  QCE_CASE(32, 16)
-  QCE_CASE(32, 32)
-  QCE_CASE(32, 64)
-  QCE_CASE(64, 16)
-  QCE_CASE(64, 32)
-  QCE_CASE(64, 64)
+  hipError_t e = hipMemsetAsync(a.yflag, 0, sizeof(int), st);
+  if (e != hipSuccess) return e;
+  {
+    const long long n = a.B * a.M * 2;
+    long long blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_y_exact, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(256), 0, st, n,
+                       reinterpret_cast<const double*>(a.y), a.y_scale, a.yflag);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  e = hipErrorInvalidValue;
+#define QCE_CASE(X, Y)                                                                                   \
+  if (a.MP == X && a.NP == Y)                                                                            \
+    e = hm ? launch_h2_t<X, Y, true>(a, out_partial, st) : launch_h2_t<X, Y, false>(a, out_partial, st);
+  QCE_H2_SHAPES(QCE_CASE)
 #undef QCE_CASE
-  return hipErrorInvalidValue;
+  if (e != hipSuccess) return e;
+  const long long tail0 = (long long)a.R * a.nwg;
+  const long long tiles = (a.B + 255) / 256;
+  if (a.L > 0 && (a.L % a.K != 0 || (tiles - tail0) * a.K > a.L)) {  // some tail tile may be cut
+    const long long b0 = tail0 * 256;
+    hipLaunchKernelGGL(k_merge_streamk, dim3((unsigned)((a.B - b0 + 3) / 4)), dim3(256), 0, st, a.B - b0, a.N, a.K, 0LL,
+                       a.L, a.pm, a.ps, a.pa, out_partial ? nullptr : a.h + b0 * a.N, a.om ? a.om + b0 : nullptr,
+                       a.os ? a.os + b0 : nullptr, a.oa ? a.oa + b0 * 2 * a.N : nullptr);
+    e = hipGetLastError();
+  }
+  return e;
 }
 
 int qce_h2_blocks_per_cu(int MP, int NP, int has_mean) {
   int n = 0;
   const void* fn = nullptr;
-#define QCE_OCC(X, Y)                                                                                     \
-  if (MP == X && NP == Y)                                                                                 \
-    fn = has_mean ? (const void*)k_est_all_h2<X, Y, true, false> : (const void*)k_est_all_h2<X, Y, false, false>;
-  QCE_OCC(16, 16) QCE_OCC(16, 32) QCE_OCC(16, 64) QCE_OCC(32, 16) QCE_OCC(32, 32) QCE_OCC(32, 64) QCE_OCC(64, 16)
-  QCE_OCC(64, 32) QCE_OCC(64, 64)
+#define QCE_OCC(X, Y) \
+  if (MP == X && NP == Y) \
+    fn = has_mean ? (const void*)k_est_all_h2<X, Y, true, false, false> : (const void*)k_est_all_h2<X, Y, false, false, false>;
+  QCE_H2_SHAPES(QCE_OCC)
 #undef QCE_OCC
   if (!fn || hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 512, 0) != hipSuccess || n < 1) n = 1;
   return n;
 }
 
-hipError_t qce_launch_merge_splits(long long B, int N, int nsplit, const double* pm, const double* ps, const float* pa,
-                                   double2* h, double* om, double* os, float* oa, hipStream_t st) {
-  hipLaunchKernelGGL(k_merge_splits, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, N, nsplit, pm, ps, pa, h, om,
-                     os, oa);
-  return hipGetLastError();
+#ifdef QCE_STAMPS
+extern "C" int qce_debug_stamps(unsigned long long* out, int n) {
+  if (n > 4096 * 64) n = 4096 * 64;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qce_stamps), sizeof(unsigned long long) * n) != hipSuccess) return 4;
+  return 0;
 }
+#endif

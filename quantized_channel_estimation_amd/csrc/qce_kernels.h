@@ -51,23 +51,29 @@ hipError_t qce_launch_select(long long B, int K, const double* lp, int mode, int
 hipError_t qce_launch_est_weighted(const QceEstArgs& a, const float* wts, double2* h, hipStream_t st);
 bool qce_shape_supported(int MP, int NP);
 
-// FP16 two-term split kernel (qce_estimate_h2.hip)
+// FP16 two-term split kernel (qce_estimate_h2.hip), stream-K scheduled
 struct QceH2Args {
   long long B;
-  int M, N, K, MP, NP, has_mean, nsplit;
+  int M, N, K, MP, NP, has_mean;
+  int nwg;      // persistent workgroups P
+  int R;        // data-parallel rounds of whole tiles
+  long long L;  // stream-K tail: work items (tile, component) per workgroup
   double y_scale;
+  int* yflag;  // device int: set when some observation is not exact in fp16 (k_y_exact)
   const double2* y;
   const char* pack;
   long long cstride;  // bytes per component
   const float* sinv;  // K x (NSL + NSW) inverse slice scales (y-scale folded in)
   const double* cconst;
+  double2* h;                  // final output (or nullptr with out_partial)
+  double *om, *os;             // partial-format output (K-shard path)
+  float* oa;
+  double *pm, *ps;             // scratch for cut tiles: nwg * 2 * 256 records
+  float* pa;
 };
 long long qce_pack_h2_stride_bytes(int MP, int NP, int has_mean);
 hipError_t qce_launch_pack_h2(int K, int M, int N, int MP, int NP, int has_mean, long long cstride, double y_scale,
                               const double2* Linv, const double2* W, const double2* q0, const double2* bvec, char* pack,
                               float* sinv, hipStream_t st);
-hipError_t qce_launch_est_h2(const QceH2Args& a, double2* h, double* pm, double* ps, float* pa, bool partial,
-                             hipStream_t st);
-hipError_t qce_launch_merge_splits(long long B, int N, int nsplit, const double* pm, const double* ps, const float* pa,
-                                   double2* h, double* om, double* os, float* oa, hipStream_t st);
+hipError_t qce_launch_est_h2(const QceH2Args& a, bool out_partial, hipStream_t st);
 int qce_h2_blocks_per_cu(int MP, int NP, int has_mean);

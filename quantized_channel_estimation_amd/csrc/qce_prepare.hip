@@ -276,6 +276,76 @@ __global__ __launch_bounds__(256) void k_chol_inv(int M, double2* __restrict__ L
   }
 }
 
+// Same factorisation with the matrix and its inverse resident in LDS (M <= 64: 2 x 64 KB), one
+// workgroup per component; the right-looking updates then cost LDS latency, not L2 round trips.
+__global__ __launch_bounds__(256) void k_chol_inv_lds(int M, const double2* __restrict__ Cr,
+                                                      double2* __restrict__ Linv, const double* __restrict__ logw,
+                                                      double* __restrict__ cconst, int* __restrict__ status) {
+  __shared__ double2 a[64 * 64];
+  __shared__ double2 x[64 * 64];
+  __shared__ double s_piv;
+  __shared__ int s_bad;
+  const int k = blockIdx.x, tid = threadIdx.x;
+  const double2* src = Cr + (long long)k * M * M;
+  for (int e = tid; e < M * M; e += 256) {
+    const int r = e / M, c = e % M;
+    a[r * 64 + c] = src[e];
+    x[r * 64 + c] = make_double2(r == c ? 1.0 : 0.0, 0.0);
+  }
+  if (tid == 0) s_bad = 0;
+  __syncthreads();
+  for (int j = 0; j < M; ++j) {
+    if (tid == 0) {
+      double ajj = a[j * 64 + j].x;
+      if (!(ajj > 0.0)) s_bad = 1;
+      ajj = sqrt(ajj);
+      a[j * 64 + j] = make_double2(ajj, 0.0);
+      s_piv = ajj;
+    }
+    __syncthreads();
+    if (s_bad) break;
+    const double piv = s_piv;
+    for (int i = j + 1 + tid; i < M; i += 256) {
+      const double2 v = a[i * 64 + j];
+      a[i * 64 + j] = make_double2(v.x / piv, v.y / piv);
+    }
+    __syncthreads();
+    const int n = M - j - 1;
+    for (int t = tid; t < n * n; t += 256) {
+      const int r = j + 1 + t / n, c = j + 1 + t % n;
+      if (c > r) continue;
+      a[r * 64 + c] = csub(a[r * 64 + c], cmulc(a[r * 64 + j], a[c * 64 + j]));
+    }
+    __syncthreads();
+  }
+  if (s_bad) {
+    if (tid == 0) status[k] = 1;
+    return;
+  }
+  for (int kk = 0; kk < M; ++kk) {
+    const double d = a[kk * 64 + kk].x;
+    for (int c = tid; c <= kk; c += 256) {
+      const double2 v = x[kk * 64 + c];
+      x[kk * 64 + c] = make_double2(v.x / d, v.y / d);
+    }
+    __syncthreads();
+    const int nr = M - kk - 1, nc = kk + 1;
+    for (int t = tid; t < nr * nc; t += 256) {
+      const int i = kk + 1 + t / nc, c = t % nc;
+      x[i * 64 + c] = csub(x[i * 64 + c], cmul(a[i * 64 + kk], x[kk * 64 + c]));
+    }
+    __syncthreads();
+  }
+  double2* dst = Linv + (long long)k * M * M;
+  for (int e = tid; e < M * M; e += 256) dst[e] = x[(e / M) * 64 + (e % M)];
+  if (tid == 0) {
+    double ld = 0.0;
+    for (int i = 0; i < M; ++i) ld += log(x[i * 64 + i].x);
+    cconst[k] = -(M * log(3.14159265358979323846)) + 2.0 * ld + logw[k];
+    status[k] = 0;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Packing of the FP32 fused-kernel tables (32x32x2 MFMA A-operand order).
 // Real embedding with interleaved (re, im): E[2i][2j]=Re, E[2i][2j+1]=-Im, E[2i+1][2j]=Im, E[2i+1][2j+1]=Re.
@@ -420,9 +490,14 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
   hipLaunchKernelGGL(k_gain_cr, dim3(K), dim3(256), 0, st, M, N, p.Cy, p.Cr, p.gain, p.A, p.means, p.means_y, p.Aeff,
                      p.kind, p.n_bits, p.quant_kind, p.delta, p.thr, p.lab);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if ((e = hipMemcpyAsync(p.Lw, p.Cr, sizeof(double2) * (size_t)K * M * M, hipMemcpyDeviceToDevice, st)) != hipSuccess)
-    return e;
-  hipLaunchKernelGGL(k_chol_inv, dim3(K), dim3(256), 0, st, M, p.Lw, p.Linv, p.logw, p.cconst, p.status);
+  if (M <= 64) {
+    hipLaunchKernelGGL(k_chol_inv_lds, dim3(K), dim3(256), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
+  } else {
+    if ((e = hipMemcpyAsync(p.Lw, p.Cr, sizeof(double2) * (size_t)K * M * M, hipMemcpyDeviceToDevice, st)) !=
+        hipSuccess)
+      return e;
+    hipLaunchKernelGGL(k_chol_inv, dim3(K), dim3(256), 0, st, M, p.Lw, p.Linv, p.logw, p.cconst, p.status);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // X = Linv Aeff (M x N) -> work
   if ((e = zgemm(0, 0, M, N, M, one, p.Linv, M, (long long)M * M, p.Aeff, N, (long long)M * N, zero, p.work, N,

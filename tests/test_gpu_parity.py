@@ -204,11 +204,11 @@ def test_device_io_torch():
     assert rel_fro(out.cpu().numpy(), host) == 0.0
 
 
-@pytest.mark.parametrize("env", [{}, {"QCE_NSPLIT": "1"}, {"QCE_NSPLIT": "3"}, {"QCE_NSPLIT": "7"},
-                                 {"QCE_KERNEL": "f32"}])
+@pytest.mark.parametrize("env", [{}, {"QCE_WORKGROUPS": "1"}, {"QCE_WORKGROUPS": "7"}, {"QCE_WORKGROUPS": "100"},
+                                 {"QCE_WORKGROUPS": "5000"}, {"QCE_KERNEL": "f32"}, {"QCE_H2_NARROW": "1"}])
 def test_all_mode_kernel_variants_vs_oracle(env, monkeypatch):
-    """FP16 two-term split kernel (default), its split-K merge, and the FP32-MFMA kernel all
-    agree with the FP64 oracle."""
+    """FP16 two-term split kernel (default) under different stream-K cuts (1 workgroup, uneven
+    cuts, more workgroups than items), and the FP32-MFMA kernel, all agree with the FP64 oracle."""
     _gpu_or_skip()
     from oracle import qce_oracle as O
     from quantized_channel_estimation_amd import Gmm_nbit
