@@ -8,8 +8,8 @@ from bench import CONFIGS, make_inputs
 from quantized_channel_estimation_amd import _lib
 
 variants = {
-    "wide": {},
-    "narrow": {"QCE_H2_NARROW": "1"},
+    "deep8": {},
+    "wide4": {"QCE_H2_WIDE": "1"},
 }
 extra = json.loads(sys.argv[1]) if len(sys.argv) > 1 else {}
 variants.update(extra)
@@ -26,7 +26,7 @@ res = {k: [] for k in variants}
 ref = None
 for rnd in range(6):
     for name, env in variants.items():
-        for k in ("QCE_H2_NARROW", "QCE_KERNEL", "QCE_WORKGROUPS"):
+        for k in ("QCE_H2_WIDE", "QCE_KERNEL", "QCE_WORKGROUPS"):
             os.environ.pop(k, None)
         os.environ.update(env)
         m.estimate(yd, out=out, stream=st.cuda_stream)

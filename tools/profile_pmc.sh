@@ -8,7 +8,7 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 BENCH="python $R/bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-parity"
 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
-run() { name=$1; shift; timeout -k 10 300 rocprofv3 --kernel-trace --pmc "$@" -d $OUT/$name -o run --output-format csv -- $BENCH > $OUT/$name.log 2>&1; }
+run() { name=$1; shift; timeout -k 10 -s KILL 150 rocprofv3 --kernel-trace --pmc "$@" -d $OUT/$name -o run --output-format csv -- $BENCH > $OUT/$name.log 2>&1; }
 run fetch FETCH_SIZE
 run write WRITE_SIZE
 run sq SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE
