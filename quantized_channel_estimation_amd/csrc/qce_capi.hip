@@ -53,6 +53,8 @@ int pad_dim(int v) {
   if (v <= 16) return 16;
   if (v <= 32) return 32;
   if (v <= 64) return 64;
+  if (v <= 128) return 128;
+  if (v <= 256) return 256;
   return -1;
 }
 
@@ -139,10 +141,15 @@ bool use_h2() {
   return !(e && strcmp(e, "f32") == 0);
 }
 
+int run_h2x(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, float* oa,
+            hipStream_t st);
+
 // 'all' mode on the FP16 split kernel, stream-K scheduled over the resident workgroups: final h,
 // or the (m, s, acc) partial when h == nullptr (K-shard path)
+
 int run_h2(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, float* oa,
            hipStream_t st) {
+  if (qce_h2x_shape(m->MP, m->NP)) return run_h2x(m, dy, B, h, om, os, oa, st);
   const long long tiles = (B + 255) / 256;
   long long slots = (long long)m->cu_count * qce_h2_blocks_per_cu(m->MP, m->NP, m->has_mean);
   const char* e = getenv("QCE_WORKGROUPS");
@@ -193,6 +200,59 @@ int run_h2(qce_model* m, const double2* dy, long long B, double2* h, double* om,
   return QCE_OK;
 }
 
+// 'all' mode for the large padded shapes (qce_estimate_h2x.hip): 128-sample tiles x K splits x
+// row chunks, split records merged by k_merge_splits
+int run_h2x(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, float* oa,
+            hipStream_t st) {
+  const long long tiles = (B + qce_h2x_tile() - 1) / qce_h2x_tile();
+  const long long nrc = qce_h2x_row_chunks(m->MP, m->NP);
+  const long long slots = m->cu_count;  // one 128 KB-LDS workgroup per CU
+  int ksplit = 1;
+  double best = 0.0;
+  for (int s = 1; s <= 8 && s <= m->K; ++s) {  // fill the chip: tiles*s*nrc over whole waves of workgroups
+    const long long wg = tiles * s * nrc;
+    const double eff = (double)wg / (double)(slots * ((wg + slots - 1) / slots));
+    if (eff > best + 0.02) {
+      best = eff;
+      ksplit = s;
+    }
+  }
+  const char* e = getenv("QCE_KSPLIT");
+  if (e && atoi(e) > 0) ksplit = atoi(e) < m->K ? atoi(e) : m->K;
+  QceH2XArgs a;
+  a.B = B;
+  a.M = m->M;
+  a.N = m->N;
+  a.K = m->K;
+  a.MP = m->MP;
+  a.NP = m->NP;
+  a.has_mean = m->has_mean;
+  a.y_scale = m->y_scale;
+  HIPCHK(m->yflag.ensure(1));
+  a.yflag = m->yflag.p;
+  a.y = dy;
+  a.pack = m->pack16.p;
+  a.cstride = m->cstride16;
+  a.sinv = m->sinv.p;
+  a.cconst = m->cconst.p;
+  a.h = h;
+  a.om = om;
+  a.os = os;
+  a.oa = oa;
+  a.rm = a.rs = nullptr;
+  a.ra = nullptr;
+  if (ksplit > 1) {
+    HIPCHK(m->sp_m.ensure((size_t)ksplit * B));
+    HIPCHK(m->sp_s.ensure((size_t)ksplit * B));
+    HIPCHK(m->sp_a.ensure((size_t)ksplit * B * 2 * m->N));
+    a.rm = m->sp_m.p;
+    a.rs = m->sp_s.p;
+    a.ra = m->sp_a.p;
+  }
+  HIPCHK(qce_launch_est_h2x(a, ksplit, h == nullptr, st));
+  return QCE_OK;
+}
+
 int check_model(qce_model* m, bool need_prepared) {
   if (!m) return fail(QCE_EARG, "null model");
   if (need_prepared && !m->prepared) return fail(QCE_ESTATE, "qce_prepare has not been called on this model");
@@ -221,7 +281,7 @@ int qce_model_create(int K, int N, const double* means_cplx, const double* covs_
   if (!out || !covs_cplx || !weights) return fail(QCE_EARG, "null argument");
   *out = nullptr;
   if (K <= 0 || N <= 0) return fail(QCE_EARG, "K and N must be positive");
-  if (pad_dim(N) < 0) return fail(QCE_ENOTIMPL, "N > 64 is not covered by the estimate kernels yet");
+  if (pad_dim(N) < 0) return fail(QCE_ENOTIMPL, "N > 256 is not covered by the estimate kernels");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(QCE_EHIP, "no HIP device visible");
   if (device < 0 || device >= ndev) return fail(QCE_EARG, "device index out of range");
@@ -294,7 +354,7 @@ int qce_prepare(qce_model* m, const double* A, int M, double snr_db, double n_bi
   const int N = m->N, K = m->K;
   if (!A) M = N;
   if (M <= 0) return fail(QCE_EARG, "M must be positive");
-  if (pad_dim(M) < 0) return fail(QCE_ENOTIMPL, "M > 64 is not covered by the estimate kernels yet");
+  if (pad_dim(M) < 0) return fail(QCE_ENOTIMPL, "M > 256 is not covered by the estimate kernels");
   int kind;
   int nb = 0;
   if (n_bits == 1.0) {
@@ -331,7 +391,11 @@ int qce_prepare(qce_model* m, const double* A, int M, double snr_db, double n_bi
   HIPCHK(m->status.ensure(K));
   HIPCHK(m->thr.ensure(256));
   HIPCHK(m->lab.ensure(256));
-  const int MP = pad_dim(M), NP = pad_dim(N);
+  int MP = pad_dim(M), NP = pad_dim(N);
+  if (MP > 64 || NP > 64) {  // the chunk-streamed kernel family (qce_estimate_h2x.hip) starts at 64
+    MP = MP < 64 ? 64 : MP;
+    NP = NP < 64 ? 64 : NP;
+  }
   const long long s32 = qce_pack_f32_stride(MP, NP, m->has_mean);
   const long long s64 = qce_pack_f64_stride(MP, m->has_mean);
   HIPCHK(m->pack32.ensure((size_t)s32 * K));
@@ -412,7 +476,7 @@ int qce_prepare(qce_model* m, const double* A, int M, double snr_db, double n_bi
   else if (kind == 1 && quant_kind == QCE_QUANT_UNIFORM && delta > 0.0) y_scale = 2.0 / delta;
   const long long cs16 = qce_pack_h2_stride_bytes(MP, NP, m->has_mean);
   const int nslices = (2 * MP) / 32 + (2 * NP) / 32;
-  HIPCHK(m->pack16.ensure((size_t)cs16 * K));
+  HIPCHK(m->pack16.ensure((size_t)cs16 * K + (size_t)qce_h2x_pad_bytes()));
   HIPCHK(m->sinv.ensure((size_t)nslices * K));
   HIPCHK(qce_launch_pack_h2(K, M, N, MP, NP, m->has_mean, cs16, y_scale, m->Linv.p, m->W.p, m->q0.p, m->bvec.p,
                             m->pack16.p, m->sinv.p, st));
@@ -444,7 +508,8 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
   if (rc) return rc;
   if (B < 0 || (B > 0 && (!y || !h_out))) return fail(QCE_EARG, "bad y / h_out");
   if (B == 0) return QCE_OK;
-  if (!qce_shape_supported(m->MP, m->NP)) return fail(QCE_ENOTIMPL, "shape not covered");
+  if (mode != QCE_MODE_ALL && !qce_select_shape_supported(m->MP, m->NP))
+    return fail(QCE_ENOTIMPL, "selective modes: shape not covered");
   if (mode != QCE_MODE_ALL && m->K > 256) return fail(QCE_ENOTIMPL, "selective modes support K <= 256");
   DeviceGuard g(m->device);
   hipStream_t st = pick_stream(m, stream);
@@ -457,7 +522,7 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
   }
   QceEstArgs a = est_args(m, dy, B);
   if (mode == QCE_MODE_ALL) {
-    if (use_h2()) {
+    if (use_h2() || !qce_shape_supported(m->MP, m->NP)) {
       if ((rc = run_h2(m, dy, B, dh, nullptr, nullptr, nullptr, st))) return rc;
     } else {
       HIPCHK(qce_launch_est_all(a, dh, st));
@@ -547,7 +612,7 @@ int qce_estimate_partial(qce_model* m, const double* y, int64_t B, double* m_out
     ds = m->s_scr.p;
     da = m->acc_scr.p;
   }
-  if (use_h2()) {
+  if (use_h2() || !qce_shape_supported(m->MP, m->NP)) {
     if ((rc = run_h2(m, dy, B, nullptr, dm, ds, da, st))) return rc;
   } else {
     QceEstArgs a = est_args(m, dy, B);

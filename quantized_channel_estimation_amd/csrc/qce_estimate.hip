@@ -147,8 +147,8 @@ __global__ __launch_bounds__(256, 2) void k_est_all_f32(long long B, int M, int 
 
 // h = sum_k w[b][k] (W_k y + b_k): the LMMSE half only, for the selective modes.  A
 // component no sample of the wave selected is skipped wave-uniformly.
-template <int MP, int NP, bool HAS_MEAN>
-__global__ __launch_bounds__(256, 2) void k_est_weighted_f32(long long B, int M, int N, int K,
+template <int MP, int NP, bool HAS_MEAN, int RC>
+__global__ __launch_bounds__(256, (MP > 64 || NP > 64) ? 1 : 2) void k_est_weighted_f32(long long B, int M, int N, int K,
                                                              const double2* __restrict__ y,
                                                              const float* __restrict__ pack, long long comp_stride,
                                                              const float* __restrict__ wts, double2* __restrict__ h) {
@@ -172,9 +172,11 @@ __global__ __launch_bounds__(256, 2) void k_est_weighted_f32(long long B, int M,
     yv[s] = v;
   }
   if (HAS_MEAN) yv[MP] = hh ? 0.0f : 1.0f;
-  f32x16 out[NSW];
+  static_assert(NSW % RC == 0, "row chunk");
+  const int r0 = blockIdx.y * RC;  // first W slice of this workgroup's row chunk
+  f32x16 out[RC];
 #pragma unroll
-  for (int r = 0; r < NSW; ++r)
+  for (int r = 0; r < RC; ++r)
 #pragma unroll
     for (int q = 0; q < 16; ++q) out[r][q] = 0.0f;
   for (int k = 0; k < K; ++k) {
@@ -182,11 +184,11 @@ __global__ __launch_bounds__(256, 2) void k_est_weighted_f32(long long B, int M,
     if (__ballot(w != 0.0f) == 0ull) continue;
     const f32x4* __restrict__ pk = reinterpret_cast<const f32x4*>(pack + (long long)k * comp_stride) + lane;
 #pragma unroll
-    for (int r = 0; r < NSW; ++r) {
+    for (int r = 0; r < RC; ++r) {
       f32x16 acc;
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
-      const int base = GL_TOTAL + r * (GW + HM);
+      const int base = GL_TOTAL + (r0 + r) * (GW + HM);
 #pragma unroll
       for (int g = 0; g < GW; ++g) {
         f32x4 a = pk[(base + g) * 64];
@@ -206,10 +208,10 @@ __global__ __launch_bounds__(256, 2) void k_est_weighted_f32(long long B, int M,
   if (!valid) return;
   double2* hp = h + sample * N;
 #pragma unroll
-  for (int r = 0; r < NSW; ++r)
+  for (int r = 0; r < RC; ++r)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int n0 = 16 * r + 4 * q + 2 * hh;
+      const int n0 = 16 * (r0 + r) + 4 * q + 2 * hh;
       if (n0 < N) hp[n0] = make_double2((double)out[r][4 * q + 0], (double)out[r][4 * q + 1]);
       if (n0 + 1 < N) hp[n0 + 1] = make_double2((double)out[r][4 * q + 2], (double)out[r][4 * q + 3]);
     }
@@ -218,7 +220,7 @@ __global__ __launch_bounds__(256, 2) void k_est_weighted_f32(long long B, int M,
 // lp[b][k] in FP64 on v_mfma_f64_16x16x4_f64 (exact argmax / ranking for the selective modes
 // and for predict_proba_cplx / _predict_cplx).  4 waves x 16 samples per workgroup.
 template <int MP, bool HAS_MEAN>
-__global__ __launch_bounds__(256, 2) void k_lp_f64(long long B, int M, int K, const double2* __restrict__ y,
+__global__ __launch_bounds__(256, MP > 64 ? 1 : 2) void k_lp_f64(long long B, int M, int K, const double2* __restrict__ y,
                                                    const double* __restrict__ pack, long long comp_stride,
                                                    const double* __restrict__ cconst, double* __restrict__ lp) {
   constexpr int R = 2 * MP;
@@ -376,9 +378,13 @@ __global__ __launch_bounds__(256) void k_select(long long B, int K, const double
 // ---------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------
-bool qce_shape_supported(int MP, int NP) {
+bool qce_shape_supported(int MP, int NP) {  // the FP32 fused 'all' kernel (k_est_all_f32)
   auto ok = [](int v) { return v == 16 || v == 32 || v == 64; };
   return ok(MP) && ok(NP);
+}
+
+bool qce_select_shape_supported(int MP, int NP) {  // lp (FP64) + weighted LMMSE kernels
+  return qce_shape_supported(MP, NP) || ((MP == 64 || MP == 128 || MP == 256) && (NP == 64 || NP == 128 || NP == 256));
 }
 
 template <int MP, int NP, bool HM>
@@ -396,8 +402,11 @@ static hipError_t launch_all_t(const QceEstArgs& a, double2* h, double* pm, doub
 
 template <int MP, int NP, bool HM>
 static hipError_t launch_w_t(const QceEstArgs& a, const float* w, double2* h, hipStream_t st) {
-  dim3 grid((unsigned)((a.B + 127) / 128));
-  hipLaunchKernelGGL((k_est_weighted_f32<MP, NP, HM>), grid, dim3(256), 0, st, a.B, a.M, a.N, a.K, a.y, a.pack32,
+  // row chunk: y (MP + 1 registers) + RC accumulator slices (16 registers each) within ~400
+  constexpr int NSW = (2 * NP) / 32;
+  constexpr int RC = (MP <= 64 && NP <= 64) ? NSW : ((MP + 16 * NSW <= 400) ? NSW : (MP + 128 <= 400 ? 8 : 4));
+  dim3 grid((unsigned)((a.B + 127) / 128), NSW / RC);
+  hipLaunchKernelGGL((k_est_weighted_f32<MP, NP, HM, RC>), grid, dim3(256), 0, st, a.B, a.M, a.N, a.K, a.y, a.pack32,
                      a.stride32, w, h);
   return hipGetLastError();
 }
@@ -435,11 +444,14 @@ hipError_t qce_launch_est_partial(const QceEstArgs& a, double* m, double* s, flo
   return hipErrorInvalidValue;
 }
 
+#define QCE_FOR_LARGE_SHAPES(X) X(64, 128) X(64, 256) X(128, 64) X(128, 128) X(128, 256) X(256, 64) X(256, 128) X(256, 256)
+
 hipError_t qce_launch_est_weighted(const QceEstArgs& a, const float* w, double2* h, hipStream_t st) {
   const bool hm = a.has_mean != 0;
 #define QCE_CASE(X, Y) \
   if (a.MP == X && a.NP == Y) return hm ? launch_w_t<X, Y, true>(a, w, h, st) : launch_w_t<X, Y, false>(a, w, h, st);
   QCE_FOR_SHAPES(QCE_CASE)
+  QCE_FOR_LARGE_SHAPES(QCE_CASE)
 #undef QCE_CASE
   return hipErrorInvalidValue;
 }
@@ -450,6 +462,8 @@ hipError_t qce_launch_lp(const QceEstArgs& a, double* lp, hipStream_t st) {
     case 16: return hm ? launch_lp_t<16, true>(a, lp, st) : launch_lp_t<16, false>(a, lp, st);
     case 32: return hm ? launch_lp_t<32, true>(a, lp, st) : launch_lp_t<32, false>(a, lp, st);
     case 64: return hm ? launch_lp_t<64, true>(a, lp, st) : launch_lp_t<64, false>(a, lp, st);
+    case 128: return hm ? launch_lp_t<128, true>(a, lp, st) : launch_lp_t<128, false>(a, lp, st);
+    case 256: return hm ? launch_lp_t<256, true>(a, lp, st) : launch_lp_t<256, false>(a, lp, st);
     default: return hipErrorInvalidValue;
   }
 }

@@ -23,40 +23,18 @@
 //    the same combine the K-shard multi-GPU path uses.
 #include "qce_common.h"
 #include "qce_kernels.h"
+#include "qce_h2_common.h"
 
 #include <stdlib.h>
 
 #include <utility>
 
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-
-#define QCE_NEG_INF (-__builtin_inf())
-
-template <int MP, int NP, bool HM>
-struct H2Geom {
-  static constexpr int R = 2 * MP, S = 2 * NP;
-  static constexpr int NSL = R / 32, NSW = S / 32;
-  static constexpr int KS = R / 16;  // k-steps of 16 real columns
-  static constexpr int HMI = HM ? 1 : 0;
-  // k-step units of 2 KB (two pieces x 64 lanes x 16 B)
-  static constexpr int GL_STEPS = NSL * (NSL + 1) + HMI * NSL;  // sum_r (2r + 2 + HM)
-  static constexpr int GW_STEPS = NSW * (KS + HMI);
-  static constexpr int GL_BYTES = GL_STEPS * 2048;
-  static constexpr int GW_BYTES = GW_STEPS * 2048;
-  static constexpr int COMP_BYTES = GL_BYTES + GW_BYTES;
-  static constexpr __host__ __device__ int gl_off(int r) { return r * (r + 1) + HMI * r; }  // in steps
-};
 
 long long qce_pack_h2_stride_bytes(int MP, int NP, int has_mean) {
   const int R = 2 * MP, S = 2 * NP, NSL = R / 32, NSW = S / 32, KS = R / 16, HMI = has_mean ? 1 : 0;
   return (long long)(NSL * (NSL + 1) + HMI * NSL + NSW * (KS + HMI)) * 2048;
 }
 
-QCE_DEV f16x8 lds_frag(const char* base, int byte_off, int lane) {
-  return *reinterpret_cast<const f16x8*>(base + byte_off + lane * 16);
-}
-
-QCE_DEV f32x16 mfma_h(f16x8 a, f16x8 b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
 
 // global -> LDS copy of `bytes` (multiple of 1 KB) by the 8 waves, one 1 KB wave-instruction each
 template <int BYTES>
@@ -102,11 +80,6 @@ __device__ unsigned long long g_qce_stamps[4096 * 8 * 8];
 #define QCE_STAMP_FLUSH
 #endif
 
-QCE_DEV void raw_barrier() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
 
 QCE_DEV int gl_slice_of(int idx, int hmi) {  // slice r holds steps [r(r+1) + hmi r, ... + 2r + 2 + hmi)
   int r = 0, base = 0;
@@ -223,21 +196,6 @@ QCE_DEV void gw_phase(const char* sw, const f16x8* yh, const f16x8* yl, const fl
   }
 }
 
-// The per-component scalars (slice scales, c_k) are fetched with scalar loads and waited for right
-// away, before the LDS reads of a phase: an outstanding SMEM load would force every later LDS wait
-// to lgkmcnt(0) (scalar loads return out of order), which serialises the fragment prefetch.
-template <int NS>
-struct CompScalars {
-  float s[NS];
-  double c;
-  QCE_DEV void load(const float* __restrict__ sinv, const double* __restrict__ cconst, int k) {
-    const float* sk = sinv + (long long)k * NS;
-#pragma unroll
-    for (int i = 0; i < NS; ++i) s[i] = sk[i];
-    c = cconst[k];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  }
-};
 
 // ---- exact-path phases with hand-counted LDS reads ---------------------------------------------
 // The fragment reads are inline-asm ds_read_b128 issued two k-steps ahead of their MFMAs and waited
@@ -245,26 +203,6 @@ struct CompScalars {
 // is scheduled above the wait, §5.7 form (ii)).  The compiler-scheduled version sank the prefetch
 // next to its use in some phases (lgkmcnt(0) before every MFMA pair).  Per-component scalars are
 // already in registers (CompScalars), so no SMEM load is in flight to disorder lgkmcnt.
-template <int OFF>
-QCE_DEV void ds_rd(f16x8& v, unsigned addr) {
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF));
-}
-template <int N_>
-QCE_DEV void wait_lgkm(f16x8& a, f16x8& b) {
-  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "i"(N_));
-}
-template <typename F, int... I>
-QCE_DEV void static_for(F&& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
-}
-constexpr int c_gl_slice(int idx, int hmi) {
-  int r = 0, base = 0;
-  while (idx >= base + 2 * r + 2 + hmi) {
-    base += 2 * r + 2 + hmi;
-    ++r;
-  }
-  return r;
-}
 
 template <int MP, int NP, bool HM>
 QCE_DEV double gl_phase_x(const char* sl, const f16x8* yh, const float* sk, int lane) {
@@ -353,13 +291,6 @@ QCE_DEV void gw_phase_x(const char* sw, const f16x8* yh, const float* sk, float 
       std::make_integer_sequence<int, NST>{});
 }
 
-QCE_DEV void softmax_step(double lp, double& m, double& ssum, float& alpha, float& p) {
-  const double mnew = fmax(m, lp);
-  alpha = (m == mnew) ? 1.0f : expf((float)(m - mnew));
-  p = (lp == QCE_NEG_INF) ? 0.0f : expf((float)(lp - mnew));
-  ssum = ssum * (double)alpha + (double)p;
-  m = mnew;
-}
 
 // Two-slot pipeline (any geometry): GL (slot L) and GW (slot W) of a component; GW_k streams in
 // during the GL phase, GL_{k+1} during the GW phase.
@@ -465,35 +396,6 @@ QCE_DEV void h2_kloop_deep(int k0, int k1, const char* __restrict__ pack, long l
   QCE_STAMP_FLUSH
 }
 
-QCE_DEV void write_final(double2* __restrict__ h, double* __restrict__ om, double* __restrict__ os,
-                         float* __restrict__ oa, long long row, int N, int hh, int NSW, const f32x16* out, double m,
-                         double ssum, bool partial_fmt) {
-  if (partial_fmt) {
-    if (hh == 0) {
-      om[row] = m;
-      os[row] = ssum;
-    }
-    float* pa = oa + row * (2LL * N);
-    for (int r = 0; r < NSW; ++r)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int n0 = 16 * r + 4 * q + 2 * hh;
-        if (n0 < N) *reinterpret_cast<float2*>(pa + 2 * n0) = make_float2(out[r][4 * q + 0], out[r][4 * q + 1]);
-        if (n0 + 1 < N)
-          *reinterpret_cast<float2*>(pa + 2 * n0 + 2) = make_float2(out[r][4 * q + 2], out[r][4 * q + 3]);
-      }
-    return;
-  }
-  const double inv = 1.0 / ssum;
-  double2* hp = h + row * N;
-  for (int r = 0; r < NSW; ++r)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int n0 = 16 * r + 4 * q + 2 * hh;
-      if (n0 < N) hp[n0] = make_double2((double)out[r][4 * q + 0] * inv, (double)out[r][4 * q + 1] * inv);
-      if (n0 + 1 < N) hp[n0 + 1] = make_double2((double)out[r][4 * q + 2] * inv, (double)out[r][4 * q + 3] * inv);
-    }
-}
 
 // Persistent data-parallel + stream-K kernel, one instance per observation class:
 // EXACT = observations exact in fp16 after the y scale (two products per MAC, no y_lo registers),
@@ -865,6 +767,13 @@ __global__ __launch_bounds__(256) void k_y_exact(long long n, const double* __re
   if (__ballot(bad) != 0ull && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
+hipError_t qce_launch_y_exact(long long n, const double* y, double y_scale, int* flag, hipStream_t st) {
+  long long blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_y_exact, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(256), 0, st, n, y, y_scale, flag);
+  return hipGetLastError();
+}
+
 // Combine the stream-K pieces of the tiles that were cut between workgroups (one wave per
 // sample; complete tiles return at once): h = sum_j acc_j e^{m_j - M} / sum_j s_j e^{m_j - M},
 // or the merged (m, s, acc) partial when h == nullptr.
@@ -1040,14 +949,9 @@ hipError_t qce_launch_est_h2(const QceH2Args& a, bool out_partial, hipStream_t s
   const bool hm = a.has_mean != 0;
   hipError_t e = hipMemsetAsync(a.yflag, 0, sizeof(int), st);
   if (e != hipSuccess) return e;
-  {
-    const long long n = a.B * a.M * 2;
-    long long blocks = (n + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(k_y_exact, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(256), 0, st, n,
-                       reinterpret_cast<const double*>(a.y), a.y_scale, a.yflag);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-  }
+  if ((e = qce_launch_y_exact(a.B * a.M * 2, reinterpret_cast<const double*>(a.y), a.y_scale, a.yflag, st)) !=
+      hipSuccess)
+    return e;
   e = hipErrorInvalidValue;
 #define QCE_CASE(X, Y)                                                                                   \
   if (a.MP == X && a.NP == Y)                                                                            \

@@ -49,7 +49,8 @@ hipError_t qce_launch_select(long long B, int K, const double* lp, int mode, int
                              long long* labels, float* wts, hipStream_t st);
 // h = sum_k wts[b][k] (W_k y_b + b_k)
 hipError_t qce_launch_est_weighted(const QceEstArgs& a, const float* wts, double2* h, hipStream_t st);
-bool qce_shape_supported(int MP, int NP);
+bool qce_shape_supported(int MP, int NP);         // FP32 fused kernel (M, N <= 64)
+bool qce_select_shape_supported(int MP, int NP);  // lp + weighted kernels of the selective modes
 
 // FP16 two-term split kernel (qce_estimate_h2.hip), stream-K scheduled
 struct QceH2Args {
@@ -77,3 +78,29 @@ hipError_t qce_launch_pack_h2(int K, int M, int N, int MP, int NP, int has_mean,
                               float* sinv, hipStream_t st);
 hipError_t qce_launch_est_h2(const QceH2Args& a, bool out_partial, hipStream_t st);
 int qce_h2_blocks_per_cu(int MP, int NP, int has_mean);
+
+// *flag |= (some y * y_scale is not exactly representable in fp16); n = doubles in y
+hipError_t qce_launch_y_exact(long long n, const double* y, double y_scale, int* flag, hipStream_t st);
+
+// chunk-streamed FP16 split kernel for padded M or N of 128 / 256 (qce_estimate_h2x.hip)
+struct QceH2XArgs {
+  long long B;
+  int M, N, K, MP, NP, has_mean;
+  double y_scale;
+  int* yflag;
+  const double2* y;
+  const char* pack;
+  long long cstride;
+  const float* sinv;
+  const double* cconst;
+  double2* h;                  // final output
+  double *om, *os;             // K-shard partial output
+  float* oa;
+  double *rm, *rs;             // split records: ksplit x B (m, s), ksplit x B x 2N acc
+  float* ra;
+};
+bool qce_h2x_shape(int MP, int NP);
+long long qce_h2x_pad_bytes();  // extra bytes the pack allocation needs (chunk overrun)
+int qce_h2x_tile();
+int qce_h2x_row_chunks(int MP, int NP);
+hipError_t qce_launch_est_h2x(const QceH2XArgs& a, int ksplit, bool out_partial, hipStream_t st);

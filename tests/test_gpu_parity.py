@@ -254,3 +254,57 @@ def test_ragged_and_tiny_batches():
         hg = g.estimate_from_y(y[:B], 5.0, N, None, "all", 1)
         ho = O.estimate(means, covs, w, y[:B], 5.0, N, None, "all", 1)
         assert rel_fro(hg, ho) < H_TOL, (B, rel_fro(hg, ho))
+
+
+# ---- large padded shapes (chunk-streamed kernel, qce_estimate_h2x.hip; FP64 lp + weighted selective modes)
+@pytest.mark.parametrize("K,N,pilots,B,n_bits,mean", [
+    (16, 128, 1, 700, 1, False),        # cfg4 geometry (N = 128), small K / B
+    (7, 100, 1, 300, 2, True),          # padded N (100 -> 128), means, 2-bit uniform
+    (5, 256, 1, 260, 1, False),         # cfg5 geometry (N = 256)
+    (6, 64, 2, 300, 1, False),          # two pilots: M = 2N = 128 over N = 64
+    (4, 128, 2, 140, 2, True),          # M = 256, N = 128
+    (5, 200, 1, 150, np.inf, True),     # inexact observations at N = 256 padding (row-chunked path)
+])
+def test_large_shapes_vs_oracle(K, N, pilots, B, n_bits, mean):
+    _gpu_or_skip()
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import Gmm_nbit, inputs
+    means, covs, w = inputs.synthetic_model(K, N, seed=K + N)
+    rng = np.random.default_rng(K * N)
+    if mean:
+        means = 0.3 * inputs.crandn(K, N, rng=rng)
+    h, _ = inputs.scm_generate(B, 1, N, rng, n_path=3)
+    h = h[:, 0, :].astype(complex)
+    A = None if pilots == 1 else inputs.get_pilot_matrix(N, pilots, n_bits)
+    qz = (None, None, None)
+    if n_bits not in (1, np.inf):
+        qz = inputs.uniform_quantizer(5.0, n_bits)
+    y = inputs.get_observation_nbit(h, 5.0, A, n_bits, qz[0], qz[1], rng=rng)
+    g = Gmm_nbit.from_params(means, covs, w)
+    for mode in ("all", 1, 3, 0.9):
+        hg = g.estimate_from_y(y, 5.0, N, A, mode, n_bits, "uniform", qz)
+        ho = O.estimate(means, covs, w, y, 5.0, N, A, mode, n_bits, "uniform", qz)
+        assert rel_fro(hg, ho) < H_TOL, (mode, rel_fro(hg, ho))
+    t = O.prepare(means, covs, np.eye(N) if A is None else A, 5.0, n_bits, "uniform", qz)
+    np.testing.assert_array_equal(g._predict_cplx(y), O.predict(y, t["means_y"], t["P"], w))
+
+
+@pytest.mark.parametrize("ksplit", ["1", "2", "3", "7"])
+def test_large_shape_k_splits_and_partials(ksplit, monkeypatch):
+    """K splits of the large-shape kernel (merged by k_merge_splits) and its K-shard partial output."""
+    _gpu_or_skip()
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import Gmm_nbit, _lib
+    from quantized_channel_estimation_amd.sharding import combine_partials_numpy
+    monkeypatch.setenv("QCE_KSPLIT", ksplit)
+    K, N, B = 20, 128, 400
+    means, covs, w, h, y, qz = _synthetic(K, N, B, 55, 1)
+    ho = O.estimate(means, covs, w, y, 5.0, N, None, "all", 1)
+    hg = Gmm_nbit.from_params(means, covs, w).estimate_from_y(y, 5.0, N, None, "all", 1)
+    assert rel_fro(hg, ho) < H_TOL
+    parts = []
+    for lo, hi in [(0, 9), (9, 20)]:
+        dm = _lib.DeviceModel(means[lo:hi], covs[lo:hi], w[lo:hi])
+        dm.prepare(None, 5.0, 1.0)
+        parts.append(dm.partial(y))
+    assert rel_fro(combine_partials_numpy(parts, N), ho) < H_TOL
