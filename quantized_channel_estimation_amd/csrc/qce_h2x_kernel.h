@@ -244,6 +244,18 @@ __global__ __launch_bounds__(256, 1) void k_est_all_h2x(long long B, int M, int 
             __builtin_amdgcn_sched_barrier(0);  // keep the step order: fragment liveness as pipelined
           },
           std::make_integer_sequence<int, NV>{});
+      // the next component's steps 0 and 1 were prefetched into buf[NV % 3], buf[(NV + 1) % 3]; the
+      // loop body reads them from buf[0], buf[1]: land them, then rotate (one drain per component)
+      if constexpr (NV % 3 != 0) {
+        constexpr int b0 = NV % 3, b1 = (NV + 1) % 3;
+        x_wait_lgkm<0>(buf[b0][0], buf[b0][1]);
+        x_wait_lgkm<0>(buf[b1][0], buf[b1][1]);
+        const f16x8 n0a = buf[b0][0], n0b = buf[b0][1], n1a = buf[b1][0], n1b = buf[b1][1];
+        buf[0][0] = n0a;
+        buf[0][1] = n0b;
+        buf[1][0] = n1a;
+        buf[1][1] = n1b;
+      }
       cur = nxt;
     }
     x_wait_vm<0>();
