@@ -35,6 +35,9 @@ CONFIGS = {
     "cfg1": dict(K=16, N=32, cov="full", n_bits=1, qtype="uniform", B=1_000, snr=5.0),
     "cfg2": dict(K=64, N=64, cov="full", n_bits=1, qtype="uniform", B=10_000, snr=5.0),
     "cfg3dense": dict(K=128, N=64, cov="circulant", n_bits=3, qtype="lloyd", B=100_000, snr=5.0),
+    "cfg4": dict(K=256, N=128, cov="full", n_bits=1, qtype="uniform", B=50_000, snr=5.0),
+    "cfg5dense": dict(K=128, N=256, cov="block-circulant", blocks=(4, 64), n_bits=2, qtype="uniform", B=100_000,
+                      snr=5.0),
 }
 
 
