@@ -55,8 +55,8 @@ int qce_device_count(int* count);
 
 /* Model parameters after `Gmm_nbit.fit` (gmm_cplx_bussgang.py:96-163): means_cplx (K,N) c128,
  * covs_cplx (K,N,N) c128, gm.weights_ (K,) f64.  Replaces the attribute bag the reference keeps in
- * its sklearn GaussianMixture (:86-94).  N <= 64 (padded internally to 16/32/64), K <= 256 for the
- * selective modes. */
+ * its sklearn GaussianMixture (:86-94).  N <= 256 (padded internally to 16/32/64/128/256), K <= 256 for
+ * the selective modes.  The structure of the covariances is detected here (qce_model_structure). */
 int qce_model_create(int K, int N, const double* means_cplx, const double* covs_cplx, const double* weights,
                      int device, qce_model** out);
 int qce_model_destroy(qce_model* model);
@@ -94,8 +94,14 @@ int qce_estimate_partial(qce_model* model, const double* y, int64_t B, double* m
 int qce_get_tables(qce_model* model, double* means_y, double* Cy, double* Cr, double* P, double* A_eff, double* W,
                    double* b, double* cconst);
 
-/* Dimensions of the prepared state: M (0 before the first prepare). */
+/* Dimensions of the prepared state (M <= 256): M (0 before the first prepare). */
 int qce_model_info(qce_model* model, int* K, int* N, int* M, int* device);
+
+/* Structure of the mixture found at creation: every C_k is block-circulant for kron(F_n1, F_n2) (n1 = 1:
+ * circulant, the fits of gmm_cplx_bussgang.py:104-133), or n1 = n2 = 0.  With A = I such a model is
+ * prepared and estimated in the Fourier domain (per-bin tables; fourier_active = 1 after such a prepare).
+ * Environment QCE_FFT=0 keeps every prepare on the dense path. */
+int qce_model_structure(qce_model* model, int* n1, int* n2, int* fourier_active);
 
 /* Device synchronisation of the model's stream (for timing and for QCE_IO_DEVICE callers). */
 int qce_synchronize(qce_model* model);

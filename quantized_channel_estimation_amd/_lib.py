@@ -38,6 +38,8 @@ SIGNATURES = {
     "qce_model_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                       ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "qce_synchronize": (ctypes.c_int, [_vp]),
+    "qce_model_structure": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                           ctypes.POINTER(ctypes.c_int)]),
 }
 
 _lib = None
@@ -205,3 +207,10 @@ class DeviceModel:
 
     def synchronize(self):
         check(load().qce_synchronize(self._h))
+
+    def structure(self):
+        """(n1, n2, fourier_active): block-circulant structure found at creation ((0, 0) if none) and
+        whether the last prepare took the Fourier-domain path (qce_fft.hip)."""
+        a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        check(load().qce_model_structure(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value

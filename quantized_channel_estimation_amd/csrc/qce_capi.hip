@@ -89,6 +89,19 @@ struct qce_model {
   DevBuf<float> sp_a;
   DevBuf<int> yflag;
   int cu_count = 256;
+  // Fourier-domain path for (block-)circulant mixtures (qce_fft.hip): structure found at creation
+  int fft_n1 = 0, fft_n2 = 0;
+  int fft_active = 0;   // the last prepare took the Fourier path (dense tables computed lazily)
+  int dense_valid = 0;  // dense tables match the last prepare
+  DevBuf<double> f_ceig, f_rinvT, f_cprime, f_wT, f_gain;
+  DevBuf<double2> f_col0, f_mspec, f_uT, f_bT;
+  DevBuf<int> f_bad;
+  // arguments of the last prepare (replayed for the dense tables qce_get_tables returns)
+  struct {
+    int M = 0, quant_kind = 0, n_levels = 0;
+    double snr_db = 0.0, n_bits = 1.0;
+    std::vector<double> thr, lab;
+  } last;
 };
 
 namespace {
@@ -253,6 +266,68 @@ int run_h2x(qce_model* m, const double2* dy, long long B, double2* h, double* om
   return QCE_OK;
 }
 
+bool fft_enabled() {
+  const char* e = getenv("QCE_FFT");
+  return !(e && e[0] == '0');
+}
+
+// Is every C_k (block-)circulant for some power-of-two split N = n1 n2?  (circulant fit:
+// gmm_cplx_bussgang.py:104-117, block-circulant fit: :118-133).  Sets fft_n1/fft_n2 and keeps the
+// eigenvalues, first columns and mean spectra for the per-SNR Fourier prepare.
+hipError_t detect_structure(qce_model* m) {
+  const int K = m->K, N = m->N;
+  m->fft_n1 = m->fft_n2 = 0;
+  if (!qce_fft_pow2(N) || N < 4 || qce_fft_tile(N, K) == 0 || K > 256) return hipSuccess;
+  hipError_t e;
+  if ((e = m->f_ceig.ensure((size_t)K * N)) != hipSuccess) return e;
+  if ((e = m->f_col0.ensure((size_t)K * N)) != hipSuccess) return e;
+  if ((e = m->f_mspec.ensure((size_t)K * N)) != hipSuccess) return e;
+  if ((e = m->f_bad.ensure(K)) != hipSuccess) return e;
+  std::vector<int> bad(K);
+  for (int n1 = 1; n1 < N; n1 *= 2) {
+    const int n2 = N / n1;
+    if ((e = qce_launch_fft_struct(K, N, n1, n2, 1e-10, m->covs.p, m->means.p, m->f_ceig.p, m->f_col0.p,
+                                   m->f_mspec.p, m->f_bad.p, m->stream)) != hipSuccess)
+      return e;
+    if ((e = hipMemcpyAsync(bad.data(), m->f_bad.p, sizeof(int) * K, hipMemcpyDeviceToHost, m->stream)) != hipSuccess)
+      return e;
+    if ((e = hipStreamSynchronize(m->stream)) != hipSuccess) return e;
+    bool ok = true;
+    for (int k = 0; k < K; ++k) ok = ok && bad[k] == 0;
+    if (ok) {
+      m->fft_n1 = n1;
+      m->fft_n2 = n2;
+      return hipSuccess;
+    }
+  }
+  m->f_ceig.release();
+  m->f_col0.release();
+  m->f_mspec.release();
+  return hipSuccess;
+}
+
+QceFftEstArgs fft_args(qce_model* m, const double2* y, long long B) {
+  QceFftEstArgs a;
+  a.B = B;
+  a.N = m->N;
+  a.n1 = m->fft_n1;
+  a.n2 = m->fft_n2;
+  a.K = m->K;
+  a.has_mean = m->has_mean;
+  a.y = y;
+  a.rinvT = m->f_rinvT.p;
+  a.uT = m->f_uT.p;
+  a.cprime = m->f_cprime.p;
+  a.wT = m->f_wT.p;
+  a.bT = m->f_bT.p;
+  a.wts = nullptr;
+  a.h = nullptr;
+  a.lp = nullptr;
+  a.om = a.os = nullptr;
+  a.oa = nullptr;
+  return a;
+}
+
 int check_model(qce_model* m, bool need_prepared) {
   if (!m) return fail(QCE_EARG, "null model");
   if (need_prepared && !m->prepared) return fail(QCE_ESTATE, "qce_prepare has not been called on this model");
@@ -317,6 +392,10 @@ int qce_model_create(int K, int N, const double* means_cplx, const double* covs_
     qce_model_destroy(m);
     return fail(QCE_EHIP, std::string("model allocation failed: ") + hipGetErrorString(e));
   }
+  if ((e = detect_structure(m)) != hipSuccess) {
+    qce_model_destroy(m);
+    return fail(QCE_EHIP, std::string("structure detection failed: ") + hipGetErrorString(e));
+  }
   *out = m;
   return QCE_OK;
 }
@@ -342,13 +421,43 @@ int qce_model_destroy(qce_model* m) {
   m->sp_s.release();
   m->sp_a.release();
   m->yflag.release();
+  for (auto* b : {&m->f_ceig, &m->f_rinvT, &m->f_cprime, &m->f_wT, &m->f_gain}) b->release();
+  for (auto* b : {&m->f_col0, &m->f_mspec, &m->f_uT, &m->f_bT}) b->release();
+  m->f_bad.release();
   if (m->stream) (void)hipStreamDestroy(m->stream);
   delete m;
   return QCE_OK;
 }
 
+static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, double n_bits, int quant_kind,
+                        const double* thresholds, const double* labels, int n_levels, void* stream, bool allow_fft);
+
 int qce_prepare(qce_model* m, const double* A, int M, double snr_db, double n_bits, int quant_kind,
                 const double* thresholds, const double* labels, int n_levels, void* stream) {
+  return prepare_impl(m, A, M, snr_db, n_bits, quant_kind, thresholds, labels, n_levels, stream, true);
+}
+
+}  // extern "C"
+
+namespace {
+// The dense tables of a prepare that took the Fourier path, computed when first asked for
+// (qce_get_tables: the reference's gm state mirror); the Fourier tables stay active.
+int ensure_dense(qce_model* m) {
+  if (!m->fft_active || m->dense_valid) return QCE_OK;
+  const int rc = prepare_impl(m, nullptr, m->last.M, m->last.snr_db, m->last.n_bits, m->last.quant_kind,
+                              m->last.thr.empty() ? nullptr : m->last.thr.data(),
+                              m->last.lab.empty() ? nullptr : m->last.lab.data(), m->last.n_levels, nullptr, false);
+  if (rc) return rc;
+  m->fft_active = 1;
+  m->dense_valid = 1;
+  return QCE_OK;
+}
+}  // namespace
+
+extern "C" {
+
+static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, double n_bits, int quant_kind,
+                        const double* thresholds, const double* labels, int n_levels, void* stream, bool allow_fft) {
   int rc = check_model(m, false);
   if (rc) return rc;
   const int N = m->N, K = m->K;
@@ -373,6 +482,91 @@ int qce_prepare(qce_model* m, const double* A, int M, double snr_db, double n_bi
   }
   DeviceGuard g(m->device);
   hipStream_t st = pick_stream(m, stream);
+  bool idA = (A == nullptr);
+  if (A && M == N) {  // an explicit identity is the same observation model
+    idA = true;
+    for (int i = 0; i < M && idA; ++i)
+      for (int j = 0; j < N; ++j) {
+        const double re = A[2 * ((size_t)i * N + j)], im = A[2 * ((size_t)i * N + j) + 1];
+        if (im != 0.0 || re != (i == j ? 1.0 : 0.0)) {
+          idA = false;
+          break;
+        }
+      }
+  }
+  m->last.M = M;
+  m->last.snr_db = snr_db;
+  m->last.n_bits = n_bits;
+  m->last.quant_kind = quant_kind;
+  m->last.n_levels = n_levels;
+  if (allow_fft) {
+    m->last.thr.assign(thresholds && kind == 1 ? thresholds : nullptr,
+                       thresholds && kind == 1 ? thresholds + (n_levels > 0 ? n_levels - 1 : 0) : nullptr);
+    m->last.lab.assign(labels && kind == 1 ? labels : nullptr, labels && kind == 1 ? labels + n_levels : nullptr);
+  }
+  if (allow_fft && idA && m->fft_n1 > 0 && fft_enabled()) {
+    // Fourier-domain prepare (qce_fft.hip): per-bin tables only
+    HIPCHK(m->f_rinvT.ensure((size_t)N * K));
+    HIPCHK(m->f_uT.ensure((size_t)N * K));
+    HIPCHK(m->f_cprime.ensure(K));
+    HIPCHK(m->f_wT.ensure((size_t)K * N));
+    HIPCHK(m->f_bT.ensure((size_t)K * N));
+    HIPCHK(m->f_gain.ensure(K));
+    HIPCHK(m->status.ensure(K));
+    HIPCHK(m->thr.ensure(256));
+    HIPCHK(m->lab.ensure(256));
+    double delta = 0.0;
+    if (kind == 1 && quant_kind == QCE_QUANT_UNIFORM) {
+      static const double tbl[9] = {0, 1.596, 0.9957, 0.5860, 0.3352, 0.1881, 0.1041, 0.0569, 0.0308};
+      delta = sqrt((1.0 + pow(10.0, -snr_db / 10.0)) / 2.0) * tbl[nb];
+    }
+    if (kind == 1 && quant_kind == QCE_QUANT_LLOYD) {
+      HIPCHK(hipMemcpyAsync(m->thr.p, thresholds, sizeof(double) * (n_levels - 1), hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(m->lab.p, labels, sizeof(double) * n_levels, hipMemcpyHostToDevice, st));
+    }
+    QceFftPrepArgs fa;
+    fa.N = N;
+    fa.n1 = m->fft_n1;
+    fa.n2 = m->fft_n2;
+    fa.K = K;
+    fa.s2 = pow(10.0, -snr_db / 10.0);
+    fa.kind = kind;
+    fa.n_bits = nb;
+    fa.quant_kind = quant_kind;
+    fa.delta = delta;
+    fa.thr = m->thr.p;
+    fa.lab = m->lab.p;
+    fa.logw = m->logw.p;
+    fa.ceig = m->f_ceig.p;
+    fa.col0 = m->f_col0.p;
+    fa.mspec = m->f_mspec.p;
+    fa.rinvT = m->f_rinvT.p;
+    fa.uT = m->f_uT.p;
+    fa.cprime = m->f_cprime.p;
+    fa.wT = m->f_wT.p;
+    fa.bT = m->f_bT.p;
+    fa.gain = m->f_gain.p;
+    fa.status = m->status.p;
+    HIPCHK(qce_launch_fft_prep(fa, st));
+    std::vector<int> status(K);
+    HIPCHK(hipMemcpyAsync(status.data(), m->status.p, sizeof(int) * K, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    m->M = N;
+    m->fft_active = 1;
+    m->dense_valid = 0;
+    for (int k = 0; k < K; ++k)
+      if (status[k]) {
+        m->prepared = 0;
+        return fail(QCE_ECHOL,
+                    "Fitting the mixture model failed because some components have ill-defined empirical covariance "
+                    "(for instance caused by singleton or collapsed samples). Try to decrease the number of "
+                    "components, or increase reg_covar.");
+      }
+    m->prepared = 1;
+    return QCE_OK;
+  }
+  m->fft_active = 0;
+  m->dense_valid = 1;
   const size_t KMM = (size_t)K * M * M, KMN = (size_t)K * M * N;
   HIPCHK(m->A.ensure((size_t)M * N));
   HIPCHK(m->Cy.ensure(KMM));
@@ -508,7 +702,7 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
   if (rc) return rc;
   if (B < 0 || (B > 0 && (!y || !h_out))) return fail(QCE_EARG, "bad y / h_out");
   if (B == 0) return QCE_OK;
-  if (mode != QCE_MODE_ALL && !qce_select_shape_supported(m->MP, m->NP))
+  if (!m->fft_active && mode != QCE_MODE_ALL && !qce_select_shape_supported(m->MP, m->NP))
     return fail(QCE_ENOTIMPL, "selective modes: shape not covered");
   if (mode != QCE_MODE_ALL && m->K > 256) return fail(QCE_ENOTIMPL, "selective modes support K <= 256");
   DeviceGuard g(m->device);
@@ -521,7 +715,33 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
     dh = m->h_scr.p;
   }
   QceEstArgs a = est_args(m, dy, B);
-  if (mode == QCE_MODE_ALL) {
+  if (m->fft_active) {  // Fourier-domain path (qce_fft.hip)
+    QceFftEstArgs fa = fft_args(m, dy, B);
+    fa.h = dh;
+    if (mode == QCE_MODE_ALL) {
+      HIPCHK(qce_launch_fft_est(fa, 0, st));
+    } else {
+      int kmode, n = 0;
+      double p = 0.0;
+      if (mode == QCE_MODE_TOPN) {
+        if (mode_param < 1.0 || mode_param != floor(mode_param)) return fail(QCE_EARG, "top-n needs an integer n >= 1");
+        n = mode_param > 1e9 ? 1000000000 : (int)mode_param;
+        kmode = (n == 1) ? 3 : 1;
+      } else if (mode == QCE_MODE_CUMP) {
+        kmode = 2;
+        p = mode_param;
+      } else {
+        return fail(QCE_EARG, "unknown mode");
+      }
+      HIPCHK(m->lp_scr.ensure((size_t)B * m->K));
+      HIPCHK(m->w_scr.ensure((size_t)B * m->K));
+      fa.lp = m->lp_scr.p;
+      HIPCHK(qce_launch_fft_est(fa, 1, st));
+      HIPCHK(qce_launch_select(B, m->K, m->lp_scr.p, kmode, n, p, nullptr, nullptr, m->w_scr.p, st));
+      fa.wts = m->w_scr.p;
+      HIPCHK(qce_launch_fft_est(fa, 2, st));
+    }
+  } else if (mode == QCE_MODE_ALL) {
     if (use_h2() || !qce_shape_supported(m->MP, m->NP)) {
       if ((rc = run_h2(m, dy, B, dh, nullptr, nullptr, nullptr, st))) return rc;
     } else {
@@ -581,7 +801,13 @@ int qce_log_prob(qce_model* m, const double* X, int64_t B, double* lp_out, doubl
     HIPCHK(m->lab_scr.ensure((size_t)B));
     dlab = m->lab_scr.p;
   }
-  HIPCHK(qce_launch_lp(a, dlp, st));
+  if (m->fft_active) {
+    QceFftEstArgs fa = fft_args(m, dx, B);
+    fa.lp = dlp;
+    HIPCHK(qce_launch_fft_est(fa, 1, st));
+  } else {
+    HIPCHK(qce_launch_lp(a, dlp, st));
+  }
   if (proba_out || labels_out) HIPCHK(qce_launch_select(B, m->K, dlp, 0, 0, 0.0, dpr, dlab, nullptr, st));
   if (io == QCE_IO_HOST) {
     if (lp_out) HIPCHK(hipMemcpyAsync(lp_out, dlp, sizeof(double) * BK, hipMemcpyDeviceToHost, st));
@@ -612,7 +838,13 @@ int qce_estimate_partial(qce_model* m, const double* y, int64_t B, double* m_out
     ds = m->s_scr.p;
     da = m->acc_scr.p;
   }
-  if (use_h2() || !qce_shape_supported(m->MP, m->NP)) {
+  if (m->fft_active) {
+    QceFftEstArgs fa = fft_args(m, dy, B);
+    fa.om = dm;
+    fa.os = ds;
+    fa.oa = da;
+    HIPCHK(qce_launch_fft_est(fa, 3, st));
+  } else if (use_h2() || !qce_shape_supported(m->MP, m->NP)) {
     if ((rc = run_h2(m, dy, B, nullptr, dm, ds, da, st))) return rc;
   } else {
     QceEstArgs a = est_args(m, dy, B);
@@ -631,6 +863,7 @@ int qce_get_tables(qce_model* m, double* means_y, double* Cy, double* Cr, double
                    double* b, double* cconst) {
   int rc = check_model(m, true);
   if (rc) return rc;
+  if ((rc = ensure_dense(m))) return rc;
   DeviceGuard g(m->device);
   hipStream_t st = m->stream;
   const int K = m->K, M = m->M, N = m->N;
@@ -668,6 +901,14 @@ int qce_model_info(qce_model* m, int* K, int* N, int* M, int* device) {
   if (N) *N = m->N;
   if (M) *M = m->prepared ? m->M : 0;
   if (device) *device = m->device;
+  return QCE_OK;
+}
+
+int qce_model_structure(qce_model* m, int* n1, int* n2, int* fourier_active) {
+  if (!m) return fail(QCE_EARG, "null model");
+  if (n1) *n1 = m->fft_n1;
+  if (n2) *n2 = m->fft_n2;
+  if (fourier_active) *fourier_active = m->prepared ? m->fft_active : 0;
   return QCE_OK;
 }
 

@@ -104,3 +104,42 @@ long long qce_h2x_pad_bytes();  // extra bytes the pack allocation needs (chunk 
 int qce_h2x_tile();
 int qce_h2x_row_chunks(int MP, int NP);
 hipError_t qce_launch_est_h2x(const QceH2XArgs& a, int ksplit, bool out_partial, hipStream_t st);
+
+// Fourier-domain path for (block-)circulant mixtures with A = I (qce_fft.hip)
+struct QceFftPrepArgs {
+  int N, n1, n2, K;
+  double s2;
+  int kind, n_bits, quant_kind;
+  double delta;
+  const double *thr, *lab, *logw, *ceig;
+  const double2 *col0, *mspec;
+  double* rinvT;   // N x K
+  double2* uT;     // N x K
+  double* cprime;  // K
+  double* wT;      // K x N
+  double2* bT;     // K x N
+  double* gain;    // K
+  int* status;     // K
+};
+struct QceFftEstArgs {
+  long long B;
+  int N, n1, n2, K, has_mean;
+  const double2* y;
+  const double* rinvT;
+  const double2* uT;
+  const double* cprime;
+  const double* wT;
+  const double2* bT;
+  const float* wts;  // selection weights (out = 2)
+  double2* h;
+  double* lp;        // out = 1
+  double *om, *os;   // out = 3
+  float* oa;
+};
+bool qce_fft_pow2(int v);
+int qce_fft_tile(int N, int K);  // 0: no tile fits (K too large)
+hipError_t qce_launch_fft_struct(int K, int N, int n1, int n2, double tol, const double2* covs, const double2* means,
+                                 double* ceig, double2* col0, double2* mspec, int* bad, hipStream_t st);
+hipError_t qce_launch_fft_prep(const QceFftPrepArgs& a, hipStream_t st);
+// out: 0 'all' h, 1 lp, 2 weighted h, 3 K-shard partial
+hipError_t qce_launch_fft_est(const QceFftEstArgs& a, int out, hipStream_t st);
