@@ -7,7 +7,11 @@ quantised observations already resident in HBM.  Default workload = the metric c
 (SURVEY.md §8(d) D2): K=128 components, N=M=64 antennas, 'full' covariances, 1-bit uniform
 quantiser, SNR 5 dB, mode 'all', B=100,000 observations per GPU.
 
-  python bench.py [--gpus N --steps K --warmup W] [--config metric|cfg1|cfg2|cfg4] [--shard batch|k]
+  python bench.py [--gpus N --steps K --warmup W] [--config metric|cfg1..cfg5|cfg3dense|cfg5dense]
+                  [--shard batch|k]
+
+cfg3 / cfg5 are (block-)circulant mixtures with A = I: they take the Fourier-domain path
+(qce_fft.hip, HBM-bound roofline); the *dense variants force the dense path (QCE_FFT=0).
 
 Multi-GPU (launched by torch.distributed.run, one rank per GPU): ``--shard batch`` (default) gives
 every rank its own B observations and the whole mixture (no data-path collective, weak scaling);
@@ -29,15 +33,19 @@ sys.path.insert(0, ROOT)
 METRIC = "channel estimates/sec + MSE vs reference; K=128 N=64 full-cov, 1/2/4/8 GPU"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
 FP16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense FP16/BF16 MFMA (spec, no sparsity)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.3 TB/s measured copy)
 
 CONFIGS = {
     "metric": dict(K=128, N=64, cov="full", n_bits=1, qtype="uniform", B=100_000, snr=5.0),
     "cfg1": dict(K=16, N=32, cov="full", n_bits=1, qtype="uniform", B=1_000, snr=5.0),
     "cfg2": dict(K=64, N=64, cov="full", n_bits=1, qtype="uniform", B=10_000, snr=5.0),
-    "cfg3dense": dict(K=128, N=64, cov="circulant", n_bits=3, qtype="lloyd", B=100_000, snr=5.0),
+    "cfg3": dict(K=128, N=64, cov="circulant", n_bits=3, qtype="lloyd", B=100_000, snr=5.0),
+    "cfg3dense": dict(K=128, N=64, cov="circulant", n_bits=3, qtype="lloyd", B=100_000, snr=5.0, dense=True),
     "cfg4": dict(K=256, N=128, cov="full", n_bits=1, qtype="uniform", B=50_000, snr=5.0),
+    "cfg5": dict(K=128, N=256, cov="block-circulant", blocks=(4, 64), n_bits=2, qtype="uniform", B=100_000,
+                 snr=5.0),
     "cfg5dense": dict(K=128, N=256, cov="block-circulant", blocks=(4, 64), n_bits=2, qtype="uniform", B=100_000,
-                      snr=5.0),
+                      snr=5.0, dense=True),
 }
 
 
@@ -88,10 +96,11 @@ def cpu_baseline(cfg, means, covs, w, y, quantizer, budget_s):
         t0 = time.perf_counter()
         O.estimate_loop(means, covs, w, y[:n], cfg["snr"], N, None, cfg["n_bits"], cfg["qtype"], quantizer)
         return time.perf_counter() - t0
-    t1, t2 = run(4), run(36)
-    per = max((t2 - t1) / 32.0, 1e-6)
-    prep = max(t1 - 4 * per, 0.0)
-    n = int(max(16, min(y.shape[0], (budget_s - prep) / per)))
+    a, b = (4, 36) if N <= 64 else (1, 3)  # N >= 128: one loop-faithful estimate costs ~0.1-2 s
+    t1, t2 = run(a), run(b)
+    per = max((t2 - t1) / (b - a), 1e-6)
+    prep = max(t1 - a * per, 0.0)
+    n = int(max(b, min(y.shape[0], (budget_s - prep) / per)))
     t0 = time.perf_counter()
     O.estimate_loop(means, covs, w, y[:n], cfg["snr"], N, None, cfg["n_bits"], cfg["qtype"], quantizer)
     dt = time.perf_counter() - t0
@@ -104,6 +113,9 @@ def cpu_baseline(cfg, means, covs, w, y, quantizer, budget_s):
 
 def main():
     args = parse()
+    cfg = dict(CONFIGS[args.config])
+    if cfg.pop("dense", False):
+        os.environ["QCE_FFT"] = "0"  # read by qce_prepare: keep the structured mixture on the dense path
     import torch
     import torch.distributed as dist
     from quantized_channel_estimation_amd import _lib
@@ -115,7 +127,6 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    cfg = dict(CONFIGS[args.config])
     if args.batch:
         cfg["B"] = args.batch
     K, N, B = cfg["K"], cfg["N"], cfg["B"]
@@ -198,31 +209,47 @@ def main():
                           mse_gpu=float(np.mean(np.abs(hg[:n_chk] - h[:n_chk]) ** 2)),
                           mse_oracle=float(np.mean(np.abs(ho - h[:n_chk]) ** 2)))
 
-    # roofline of the dominant kernel (the fused estimate kernel + its stream-K merge)
+    # roofline of the dominant kernel
     k_local = K if args.shard == "batch" else (lambda s: s[1] - s[0])(component_slices(K, world)[rank])
-    flops_per_launch = 16.0 * k_local * N * N * B  # 16 K M N real flops / estimate (algorithmic)
-    achieved = flops_per_launch / (kern_ms * 1e-3) / 1e12
+    dm = model if args.shard == "batch" else shard.dev
+    fourier = bool(dm.structure()[2])
     f32_kernel = os.environ.get("QCE_KERNEL") == "f32"
-    peak = FP32_MFMA_PEAK_TFLOPS if f32_kernel else FP16_MFMA_PEAK_TFLOPS
-    # executed MFMA work: lower-triangular tiles of E(Linv) skipped (R/32 slices of 32x16 tiles) and,
-    # for the fp16 kernel, two products (hi, lo) per fp32-class MAC
-    nsl = (2 * N) // 32
-    tri = (sum(2 * r + 2 for r in range(nsl)) / (nsl * 2 * nsl) + 1.0) / 2.0
-    executed = flops_per_launch * tri * (1.0 if f32_kernel else 2.0)
     traffic = None
+    kern_tag = "fft" if fourier else ("f32" if f32_kernel else "h2")
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
-            if tj.get("config") == args.config and tj.get("B") == B and tj.get("kernel") == ("f32" if f32_kernel else "h2"):
+            if tj.get("config") == args.config and tj.get("B") == B and tj.get("kernel") == kern_tag:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=peak, unit="TFLOP/s",
-                    frac=round(achieved / peak, 4), traffic=traffic,
-                    kernel=("k_est_all_f32" if f32_kernel else "k_est_all_h2+k_merge_streamk"),
-                    peak_dtype="fp32 MFMA" if f32_kernel else "fp16 MFMA (dense)",
-                    kernel_ms=round(kern_ms, 4), flops_per_launch=flops_per_launch,
-                    mfma_issue_frac=round(executed / (kern_ms * 1e-3) / 1e12 / peak, 4))
+    if fourier:
+        # HBM-bound: 16 M bytes of y in + 16 N bytes of h out per estimate (c128)
+        bytes_per_launch = 32.0 * N * B
+        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        n1, n2, _ = dm.structure()
+        fft_flops = (4.0 * k_local * N + 10.0 * N * math.log2(N)) * B  # D3: zero-mean FFT-path flops
+        roofline = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                        kernel="k_fft_est", structure=f"block-circulant ({n1},{n2})" if n1 > 1 else "circulant",
+                        kernel_ms=round(kern_ms, 4), bytes_per_launch=bytes_per_launch,
+                        fp64_flops_per_launch=fft_flops,
+                        fp64_tflops=round(fft_flops / (kern_ms * 1e-3) / 1e12, 3))
+    else:
+        flops_per_launch = 16.0 * k_local * N * N * B  # 16 K M N real flops / estimate
+        achieved = flops_per_launch / (kern_ms * 1e-3) / 1e12
+        peak = FP32_MFMA_PEAK_TFLOPS if f32_kernel else FP16_MFMA_PEAK_TFLOPS
+        # executed MFMA work: lower-triangular tiles of E(Linv) skipped (R/32 slices of 32x16 tiles) and,
+        # for the fp16 kernel, two products (hi, lo) per fp32-class MAC
+        nsl = (2 * N) // 32
+        tri = (sum(2 * r + 2 for r in range(nsl)) / (nsl * 2 * nsl) + 1.0) / 2.0
+        executed = flops_per_launch * tri * (1.0 if f32_kernel else 2.0)
+        roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=peak, unit="TFLOP/s",
+                        frac=round(achieved / peak, 4), traffic=traffic,
+                        kernel=("k_est_all_f32" if f32_kernel else "k_est_all_h2+k_merge_streamk"),
+                        peak_dtype="fp32 MFMA" if f32_kernel else "fp16 MFMA (dense)",
+                        kernel_ms=round(kern_ms, 4), flops_per_launch=flops_per_launch,
+                        mfma_issue_frac=round(executed / (kern_ms * 1e-3) / 1e12 / peak, 4))
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -240,8 +267,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if args.shard == "batch" else "strong",
             "vs_baseline": None,
-            "dtype": "f32" if os.environ.get("QCE_KERNEL") == "f32" else "f16x2 (fp16 hi+lo split, fp32 accumulate, fp64 softmax)",
-            "data": "synthetic: SCM-Toeplitz covariances (seeded), SCM channel pool + fresh CN noise, 1-bit quantised",
+            "dtype": "f64" if fourier else ("f32" if f32_kernel else
+                                            "f16x2 (fp16 hi+lo split, fp32 accumulate, fp64 softmax)"),
+            "data": f"synthetic: seeded {cfg['cov']} SCM-derived covariances, SCM channel pool + fresh CN noise, "
+                    f"{cfg['n_bits']}-bit {cfg['qtype']} quantised",
             "config": {"workload": f"estimate_from_y K={K} N=M={N} cov={cfg['cov']} n_bits={cfg['n_bits']} "
                                    f"{cfg['qtype']} snr={cfg['snr']}dB mode=all B={B}/GPU prepare-per-step",
                        "K": K, "N": N, "B_per_gpu": B, "shard": args.shard,
