@@ -96,6 +96,8 @@ struct qce_model {
   DevBuf<double> f_ceig, f_rinvT, f_cprime, f_wT, f_gain;
   DevBuf<double2> f_col0, f_mspec, f_uT, f_bT;
   DevBuf<int> f_bad;
+  DevBuf<double> f_pr, f_pur, f_pui, f_pc, f_pw, f_pbr, f_pbi;  // qce_fft_mfma.hip tables
+  int fft_mfma = 0;                                            // the MFMA kernel serves 'all' / partial
   // arguments of the last prepare (replayed for the dense tables qce_get_tables returns)
   struct {
     int M = 0, quant_kind = 0, n_levels = 0;
@@ -325,7 +327,21 @@ QceFftEstArgs fft_args(qce_model* m, const double2* y, long long B) {
   a.lp = nullptr;
   a.om = a.os = nullptr;
   a.oa = nullptr;
+  a.Kp = qce_fft_kpad(m->K);
+  a.pr = m->f_pr.p;
+  a.pur = m->f_pur.p;
+  a.pui = m->f_pui.p;
+  a.pc = m->f_pc.p;
+  a.pw = m->f_pw.p;
+  a.pbr = m->f_pbr.p;
+  a.pbi = m->f_pbi.p;
   return a;
+}
+
+// QCE_FFT_KERNEL=lds keeps 'all' / partial on the LDS-tiled FP64 kernel of qce_fft.hip (A/B runs)
+bool fft_mfma_enabled() {
+  const char* e = getenv("QCE_FFT_KERNEL");
+  return !(e && strcmp(e, "lds") == 0);
 }
 
 int check_model(qce_model* m, bool need_prepared) {
@@ -548,6 +564,22 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
     fa.gain = m->f_gain.p;
     fa.status = m->status.p;
     HIPCHK(qce_launch_fft_prep(fa, st));
+    m->fft_mfma = 0;
+    if (qce_fft_mfma_shape(N) && fft_mfma_enabled()) {
+      const size_t KpN = (size_t)qce_fft_kpad(K) * N;
+      HIPCHK(m->f_pr.ensure(KpN));
+      HIPCHK(m->f_pc.ensure((size_t)qce_fft_kpad(K)));
+      HIPCHK(m->f_pw.ensure(KpN));
+      if (m->has_mean) {
+        HIPCHK(m->f_pur.ensure(KpN));
+        HIPCHK(m->f_pui.ensure(KpN));
+        HIPCHK(m->f_pbr.ensure(KpN));
+        HIPCHK(m->f_pbi.ensure(KpN));
+      }
+      QceFftEstArgs pa = fft_args(m, nullptr, 0);
+      HIPCHK(qce_launch_fft_pack(pa, m->f_rinvT.p, m->f_uT.p, m->f_cprime.p, m->f_wT.p, m->f_bT.p, st));
+      m->fft_mfma = 1;
+    }
     std::vector<int> status(K);
     HIPCHK(hipMemcpyAsync(status.data(), m->status.p, sizeof(int) * K, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -719,7 +751,8 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
     QceFftEstArgs fa = fft_args(m, dy, B);
     fa.h = dh;
     if (mode == QCE_MODE_ALL) {
-      HIPCHK(qce_launch_fft_est(fa, 0, st));
+      if (m->fft_mfma) HIPCHK(qce_launch_fft_mfma(fa, 0, st));
+      else HIPCHK(qce_launch_fft_est(fa, 0, st));
     } else {
       int kmode, n = 0;
       double p = 0.0;
@@ -843,7 +876,8 @@ int qce_estimate_partial(qce_model* m, const double* y, int64_t B, double* m_out
     fa.om = dm;
     fa.os = ds;
     fa.oa = da;
-    HIPCHK(qce_launch_fft_est(fa, 3, st));
+    if (m->fft_mfma) HIPCHK(qce_launch_fft_mfma(fa, 3, st));
+    else HIPCHK(qce_launch_fft_est(fa, 3, st));
   } else if (use_h2() || !qce_shape_supported(m->MP, m->NP)) {
     if ((rc = run_h2(m, dy, B, nullptr, dm, ds, da, st))) return rc;
   } else {

@@ -1,0 +1,388 @@
+// MFMA Fourier-domain 'all' / K-shard-partial estimate for (block-)circulant mixtures with A = I
+// (the per-bin algebra is derived in qce_fft.hip's header).
+//
+// Per estimate (zero mean): Y = DFT(y); lp_k = c'_k - sum_i |Y_i|^2 rinv_ik; gamma = softmax(lp);
+// f_i = sum_k gamma_k w_ki; h = IDFT(Y . f (+ sum_k gamma_k bb_ki)).  The two K x N products are the
+// whole of the arithmetic (4 K N flops per estimate) and run here on v_mfma_f64_16x16x4_f64, so the
+// result keeps the FP64 accuracy of the reference (gmm_cplx_bussgang.py computes in complex128).
+//
+// Workgroup = 4 waves and TS = 4096 / N observations (64 for N <= 64): the tile of spectra (TS x N
+// complex128 = 64 KB) sits in LDS, two workgroups per CU.  Wave w owns 16 observations (MFMA columns)
+// and a range of NB = min(N, 64) bins: for N > 64 the KW = N / 64 waves of one observation group
+// split the bins and add their partial log-probabilities through LDS (fixed order, so every wave sees
+// bit-identical lp).  Components stream in blocks of 16 (MFMA rows) with an online softmax:
+//   lp block   D[comp][obs]  = sum_bins (-rinv)[bin][comp] * |Y|^2[bin][obs]       (A: table, B: LDS)
+//   filter     F[bin][obs]  += w[comp][bin] * e^{lp - m}[comp][obs]                (B: the lp tile as is)
+// The f64 D layout (row = lane/16 + 4 r, col = lane % 16) is exactly the B-operand layout of k-step r
+// (k = lane / 16), so the softmax weights feed the filter product with no data movement.
+//
+// FFTs: radix-2 DIF in LDS grouped into radix-8/4/2 register passes (natural order in, per-axis
+// bit-reversed order out), the inverse is the exact reverse (DIT, conjugate twiddles), so no
+// bit-reversal pass exists: the per-bin tables are stored in that bit-reversed order (k_fft_pack).
+#include "qce_common.h"
+#include "qce_kernels.h"
+
+namespace {
+
+constexpr double SQH = 0.70710678118654752440;  // sqrt(1/2)
+
+QCE_DEV int brev(int j, int lg) { return lg == 0 ? 0 : (int)(__brev((unsigned)j) >> (32 - lg)); }
+
+// v * e^{-2 pi i mm / P} (INV: e^{+...}); P in {2, 4, 8}, mm < P / 2 (compile-time after unrolling)
+template <bool INV>
+QCE_DEV double2 rootmul(double2 v, int P, int mm) {
+  if (mm == 0) return v;
+  if (P == 4 || mm == 2) return INV ? make_double2(-v.y, v.x) : make_double2(v.y, -v.x);
+  if (mm == 1)
+    return INV ? make_double2((v.x - v.y) * SQH, (v.x + v.y) * SQH) : make_double2((v.x + v.y) * SQH, (v.y - v.x) * SQH);
+  return INV ? make_double2((-v.x - v.y) * SQH, (v.x - v.y) * SQH) : make_double2((v.y - v.x) * SQH, (-v.x - v.y) * SQH);
+}
+
+// One register pass of RL radix-2 stages over every line of one axis of every observation row.
+// Axis length L = 2^lgL, element stride st (1: the n2 axis, n2: the n1 axis), first half-distance
+// D = 2^lgD (axis units).  A group holds R = 2^RL elements a_m = blk 2D + j + m E (E = 2D / R).
+// Forward (DIF): stage s pairs (m, m + R/2^{s+1}) with twiddle W_{2D_s}^{j + (m mod half) E}.
+// Inverse (DIT): the same stages in reverse order, conjugate twiddles.
+template <int RL, bool INV>
+QCE_DEV void fft_pass(double2* T, int lgTS, int RS, int lgN, int lgL, int st, int lgD, const double2* tw) {
+  constexpr int R = 1 << RL;
+  const int lgE = lgD + 1 - RL;
+  const int lgnb = lgL - lgD - 1;  // blocks per line
+  const int total = 1 << (lgTS + lgN - RL);
+  const int TSm = (1 << lgTS) - 1;
+  for (int it = threadIdx.x; it < total; it += 256) {
+    const int s = it & TSm, q = it >> lgTS;
+    const int j = q & ((1 << lgE) - 1), rest = q >> lgE;
+    const int blk = rest & ((1 << lgnb) - 1), line = rest >> lgnb;
+    double2* row = T + s * RS;
+    int idx[R];
+    double2 x[R];
+#pragma unroll
+    for (int m = 0; m < R; ++m) {
+      const int a = (blk << (lgD + 1)) + j + (m << lgE);
+      idx[m] = (st == 1) ? (line << lgL) + a : a * st + line;
+      x[m] = row[idx[m]];
+    }
+    double2 w[RL];
+#pragma unroll
+    for (int sI = 0; sI < RL; ++sI) {  // W_{2 D_s}^j = tw[j * 128 / D_s]
+      w[sI] = tw[j << (7 - (lgD - sI))];
+      if (INV) w[sI].y = -w[sI].y;
+    }
+    if (!INV) {
+#pragma unroll
+      for (int sI = 0; sI < RL; ++sI) {
+        const int half = R >> (sI + 1);
+#pragma unroll
+        for (int m = 0; m < R; ++m) {
+          if (m & half) continue;
+          const double2 a = x[m], b = x[m + half];
+          x[m] = cadd(a, b);
+          x[m + half] = rootmul<false>(cmul(csub(a, b), w[sI]), 2 * half, m & (half - 1));
+        }
+      }
+    } else {
+#pragma unroll
+      for (int sI = RL - 1; sI >= 0; --sI) {
+        const int half = R >> (sI + 1);
+#pragma unroll
+        for (int m = 0; m < R; ++m) {
+          if (m & half) continue;
+          const double2 a = x[m];
+          const double2 b = rootmul<true>(cmul(x[m + half], w[sI]), 2 * half, m & (half - 1));
+          x[m] = cadd(a, b);
+          x[m + half] = csub(a, b);
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < R; ++m) row[idx[m]] = x[m];
+  }
+}
+
+template <bool INV>
+QCE_DEV void fft_axis_passes(double2* T, int lgTS, int RS, int lgN, int lgL, int st, const double2* tw) {
+  // forward: half-distances L/2 .. 1 in groups of <= 3 stages; inverse: the same passes reversed
+  int rl[3], dd[3], np = 0;
+  for (int rem = lgL, lgD = lgL - 1; rem > 0;) {
+    const int r = rem < 3 ? rem : 3;
+    rl[np] = r;
+    dd[np] = lgD;
+    ++np;
+    lgD -= r;
+    rem -= r;
+  }
+  for (int i = 0; i < np; ++i) {
+    const int p = INV ? np - 1 - i : i;
+    if (rl[p] == 3) fft_pass<3, INV>(T, lgTS, RS, lgN, lgL, st, dd[p], tw);
+    else if (rl[p] == 2) fft_pass<2, INV>(T, lgTS, RS, lgN, lgL, st, dd[p], tw);
+    else fft_pass<1, INV>(T, lgTS, RS, lgN, lgL, st, dd[p], tw);
+    __syncthreads();
+  }
+}
+
+template <int N, int OUT, bool has_mean>
+__global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int lg2, int Kp,
+                                                     const double2* __restrict__ y, const double* __restrict__ pr,
+                                                     const double* __restrict__ pur, const double* __restrict__ pui,
+                                                     const double* __restrict__ pc, const double* __restrict__ pw,
+                                                     const double* __restrict__ pbr, const double* __restrict__ pbi,
+                                                     double2* __restrict__ h, double* __restrict__ om,
+                                                     double* __restrict__ os, float* __restrict__ oa) {
+  constexpr int KW = N >= 64 ? N / 64 : 1;  // waves splitting the bins of one observation group
+  constexpr int SG = 4 / KW;                // observation groups (of 16) per workgroup
+  constexpr int TS = 16 * SG;
+  constexpr int NB = N / KW;  // bins per wave
+  constexpr int NT = NB / 16;
+  constexpr int RS = N + 1;  // padded row: consecutive rows start 4 banks apart
+  constexpr int lgN = __builtin_ctz(N), lgTS = __builtin_ctz(TS);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double2* tw = reinterpret_cast<double2*>(smem);
+  double2* T = tw + 128;
+  double* X = reinterpret_cast<double*>(T + TS * RS);  // KW > 1: partial lp tiles [SG][KW][4][64]
+  const int tid = threadIdx.x;
+  const long long b0 = (long long)blockIdx.x * TS;
+  const int rows = (int)((B - b0) < TS ? (B - b0) : TS);
+
+  for (int t = tid; t < 128; t += 256) {
+    double sn, cs;
+    sincospi(-(double)t / 128.0, &sn, &cs);
+    tw[t] = make_double2(cs, sn);
+  }
+  {
+    const double2* yt = y + b0 * N;
+#pragma unroll 4
+    for (int e = tid; e < TS * N; e += 256) {
+      const int r = e >> lgN;
+      T[r * RS + (e & (N - 1))] = (r < rows) ? yt[e] : make_double2(0.0, 0.0);
+    }
+  }
+  __syncthreads();
+  const int n1 = 1 << lg1, n2 = 1 << lg2;
+  fft_axis_passes<false>(T, lgTS, RS, lgN, lg2, 1, tw);
+  if (lg1 > 0) fft_axis_passes<false>(T, lgTS, RS, lgN, lg1, n2, tw);
+
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int sg = wid % SG, kw = wid / SG;
+  const int col = lane & 15, hq = lane >> 4;
+  const int srow = sg * 16 + col;
+  double2* Trow = T + srow * RS;
+  const int bin0 = kw * NB;
+  constexpr int NTM = has_mean ? NT : 1;
+  f64x4 F[NT], Br[NTM], Bi[NTM];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+    for (int r = 0; r < 4; ++r) F[t][r] = 0.0;
+#pragma unroll
+  for (int t = 0; t < NTM; ++t)
+    for (int r = 0; r < 4; ++r) Br[t][r] = Bi[t][r] = 0.0;
+  double m = -__builtin_inf(), ssum = 0.0;
+  const int ncb = Kp >> 4;
+  for (int cb = 0; cb < ncb; ++cb) {
+    const int c0 = cb << 4;
+    f64x4 C;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) C[r] = (kw == 0) ? pc[c0 + hq + 4 * r] : 0.0;
+    {
+      const long long o = (long long)(bin0 + hq) * Kp + c0 + col;
+      const double* pa = pr + o;
+#pragma unroll
+      for (int t = 0; t < NB / 4; ++t) {
+        const double2 v = Trow[bin0 + 4 * t + hq];
+        C = mfma16x16x4d(pa[(long long)4 * t * Kp], v.x * v.x + v.y * v.y, C);
+      }
+      if constexpr (has_mean) {
+        const double *qa = pur + o, *qb = pui + o;
+#pragma unroll
+        for (int t = 0; t < NB / 4; ++t) {
+          const double2 v = Trow[bin0 + 4 * t + hq];
+          C = mfma16x16x4d(qa[(long long)4 * t * Kp], v.x, C);
+          C = mfma16x16x4d(qb[(long long)4 * t * Kp], v.y, C);
+        }
+      }
+    }
+    if constexpr (KW > 1) {  // add the bin-range partials of the KW waves of this observation group
+      double* xs = X + (sg * KW + kw) * 256 + lane;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) xs[r * 64] = C[r];
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double acc = X[(sg * KW) * 256 + r * 64 + lane];
+#pragma unroll
+        for (int q = 1; q < KW; ++q) acc += X[(sg * KW + q) * 256 + r * 64 + lane];
+        C[r] = acc;
+      }
+      __syncthreads();
+    }
+    // online softmax over this block of 16 components (rows hq + 4 r of the tile, all 4 lane groups)
+    double bm = fmax(fmax(C[0], C[1]), fmax(C[2], C[3]));
+    bm = fmax(bm, __shfl_xor(bm, 16));
+    bm = fmax(bm, __shfl_xor(bm, 32));
+    const double mn = fmax(m, bm);
+    double e[4], alpha = 1.0;
+    if (mn == -__builtin_inf()) {
+      e[0] = e[1] = e[2] = e[3] = 0.0;
+    } else {
+      alpha = exp(m - mn);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) e[r] = exp(C[r] - mn);
+    }
+    double ls = (e[0] + e[1]) + (e[2] + e[3]);
+    ls += __shfl_xor(ls, 16);
+    ls += __shfl_xor(ls, 32);
+    ssum = ssum * alpha + ls;
+    m = mn;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) F[t] *= alpha;
+    if constexpr (has_mean) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        Br[t] *= alpha;
+        Bi[t] *= alpha;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long long o = (long long)(c0 + hq + 4 * r) * N + bin0 + col;
+      const double* wa = pw + o;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) F[t] = mfma16x16x4d(wa[16 * t], e[r], F[t]);
+      if constexpr (has_mean) {
+        const double *ba = pbr + o, *bb = pbi + o;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          Br[t] = mfma16x16x4d(ba[16 * t], e[r], Br[t]);
+          Bi[t] = mfma16x16x4d(bb[16 * t], e[r], Bi[t]);
+        }
+      }
+    }
+  }
+  // Z = Y f + bb in place (each (observation, bin) of the tile belongs to exactly one lane)
+  const double sc = (OUT == 0) ? 1.0 / ssum : 1.0;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int bin = bin0 + 16 * t + hq + 4 * r;
+      const double2 v = Trow[bin];
+      const double f = F[t][r] * sc;
+      if constexpr (has_mean)
+        Trow[bin] = make_double2(fma(v.x, f, Br[t][r] * sc), fma(v.y, f, Bi[t][r] * sc));
+      else
+        Trow[bin] = make_double2(v.x * f, v.y * f);
+    }
+  if (OUT == 3 && kw == 0 && hq == 0 && srow < rows) {
+    om[b0 + srow] = m;
+    os[b0 + srow] = ssum;
+  }
+  __syncthreads();
+  if (lg1 > 0) fft_axis_passes<true>(T, lgTS, RS, lgN, lg1, n2, tw);
+  fft_axis_passes<true>(T, lgTS, RS, lgN, lg2, 1, tw);
+  (void)n1;
+  if (OUT == 3) {
+    float2* at = reinterpret_cast<float2*>(oa) + b0 * N;
+#pragma unroll 4
+    for (int e = tid; e < rows * N; e += 256) {
+      const double2 v = T[(e >> lgN) * RS + (e & (N - 1))];
+      at[e] = make_float2((float)v.x, (float)v.y);
+    }
+    return;
+  }
+  double2* ht = h + b0 * N;
+#pragma unroll 4
+  for (int e = tid; e < rows * N; e += 256) ht[e] = T[(e >> lgN) * RS + (e & (N - 1))];
+}
+
+// natural-order per-bin tables of k_fft_prep -> the kernel's storage order (bit-reversed per axis),
+// negated rinv, components padded to Kp (padding: c' = -inf, zero tables)
+__global__ __launch_bounds__(256) void k_fft_pack(int N, int lg1, int lg2, int K, int Kp, int has_mean,
+                                                  const double* __restrict__ rinvT, const double2* __restrict__ uT,
+                                                  const double* __restrict__ cprime, const double* __restrict__ wT,
+                                                  const double2* __restrict__ bT, double* __restrict__ pr,
+                                                  double* __restrict__ pur, double* __restrict__ pui,
+                                                  double* __restrict__ pc, double* __restrict__ pw,
+                                                  double* __restrict__ pbr, double* __restrict__ pbi) {
+  const int n2m = (1 << lg2) - 1;
+  auto bin_of = [&](int p) { return (brev(p >> lg2, lg1) << lg2) | brev(p & n2m, lg2); };
+  const long long total = (long long)N * Kp;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
+    {  // N x Kp
+      const int p = (int)(e / Kp), k = (int)(e % Kp);
+      const bool ok = k < K;
+      const long long src = (long long)bin_of(p) * K + k;
+      pr[e] = ok ? -rinvT[src] : 0.0;
+      if (has_mean) {
+        pur[e] = ok ? 2.0 * uT[src].x : 0.0;
+        pui[e] = ok ? 2.0 * uT[src].y : 0.0;
+      }
+    }
+    {  // Kp x N
+      const int k = (int)(e / N), p = (int)(e % N);
+      const bool ok = k < K;
+      const long long src = (long long)k * N + bin_of(p);
+      pw[e] = ok ? wT[src] : 0.0;
+      if (has_mean) {
+        pbr[e] = ok ? bT[src].x : 0.0;
+        pbi[e] = ok ? bT[src].y : 0.0;
+      }
+    }
+    if (e < Kp) pc[e] = e < K ? cprime[e] : -__builtin_inf();
+  }
+}
+
+template <int N, int OUT, bool HM>
+hipError_t launch_mfma_t(const QceFftEstArgs& a, hipStream_t st) {
+  constexpr int KW = N >= 64 ? N / 64 : 1;
+  constexpr int TS = 16 * (4 / KW);
+  const size_t lds = 128 * 16 + (size_t)TS * (N + 1) * 16 + (KW > 1 ? (size_t)(4 / KW) * KW * 256 * 8 : 0);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_fft_mfma<N, OUT, HM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int lg1 = __builtin_ctz(a.n1), lg2 = __builtin_ctz(a.n2);
+  dim3 grid((unsigned)((a.B + TS - 1) / TS));
+  hipLaunchKernelGGL((k_fft_mfma<N, OUT, HM>), grid, dim3(256), lds, st, a.B, lg1, lg2, a.Kp, a.y, a.pr,
+                     a.pur, a.pui, a.pc, a.pw, a.pbr, a.pbi, a.h, a.om, a.os, a.oa);
+  return hipGetLastError();
+}
+
+template <int OUT, bool HM>
+hipError_t launch_mfma_out(const QceFftEstArgs& a, hipStream_t st) {
+  switch (a.N) {
+    case 16: return launch_mfma_t<16, OUT, HM>(a, st);
+    case 32: return launch_mfma_t<32, OUT, HM>(a, st);
+    case 64: return launch_mfma_t<64, OUT, HM>(a, st);
+    case 128: return launch_mfma_t<128, OUT, HM>(a, st);
+    case 256: return launch_mfma_t<256, OUT, HM>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace
+
+bool qce_fft_mfma_shape(int N) { return N >= 16 && N <= 256 && (N & (N - 1)) == 0; }
+
+int qce_fft_kpad(int K) { return (K + 15) & ~15; }
+
+hipError_t qce_launch_fft_pack(const QceFftEstArgs& a, const double* rinvT, const double2* uT, const double* cprime,
+                               const double* wT, const double2* bT, hipStream_t st) {
+  const int lg1 = __builtin_ctz(a.n1), lg2 = __builtin_ctz(a.n2);
+  const long long total = (long long)a.N * a.Kp;
+  const int blocks = (int)((total + 255) / 256);
+  hipLaunchKernelGGL(k_fft_pack, dim3(blocks), dim3(256), 0, st, a.N, lg1, lg2, a.K, a.Kp, a.has_mean, rinvT, uT,
+                     cprime, wT, bT, const_cast<double*>(a.pr), const_cast<double*>(a.pur),
+                     const_cast<double*>(a.pui), const_cast<double*>(a.pc), const_cast<double*>(a.pw),
+                     const_cast<double*>(a.pbr), const_cast<double*>(a.pbi));
+  return hipGetLastError();
+}
+
+hipError_t qce_launch_fft_mfma(const QceFftEstArgs& a, int out, hipStream_t st) {
+  if (a.B <= 0) return hipSuccess;
+  if (out == 0) return a.has_mean ? launch_mfma_out<0, true>(a, st) : launch_mfma_out<0, false>(a, st);
+  if (out == 3) return a.has_mean ? launch_mfma_out<3, true>(a, st) : launch_mfma_out<3, false>(a, st);
+  return hipErrorInvalidValue;
+}

@@ -135,6 +135,9 @@ struct QceFftEstArgs {
   double* lp;        // out = 1
   double *om, *os;   // out = 3
   float* oa;
+  // MFMA kernel tables (qce_fft_mfma.hip, storage order, components padded to Kp)
+  int Kp;
+  const double *pr, *pur, *pui, *pc, *pw, *pbr, *pbi;
 };
 bool qce_fft_pow2(int v);
 int qce_fft_tile(int N, int K);  // 0: no tile fits (K too large)
@@ -143,3 +146,9 @@ hipError_t qce_launch_fft_struct(int K, int N, int n1, int n2, double tol, const
 hipError_t qce_launch_fft_prep(const QceFftPrepArgs& a, hipStream_t st);
 // out: 0 'all' h, 1 lp, 2 weighted h, 3 K-shard partial
 hipError_t qce_launch_fft_est(const QceFftEstArgs& a, int out, hipStream_t st);
+// MFMA Fourier kernel (qce_fft_mfma.hip): N in {16, ..., 256}; out 0 'all' h, 3 K-shard partial
+bool qce_fft_mfma_shape(int N);
+int qce_fft_kpad(int K);
+hipError_t qce_launch_fft_pack(const QceFftEstArgs& a, const double* rinvT, const double2* uT, const double* cprime,
+                               const double* wT, const double2* bT, hipStream_t st);
+hipError_t qce_launch_fft_mfma(const QceFftEstArgs& a, int out, hipStream_t st);

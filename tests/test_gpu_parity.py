@@ -399,3 +399,43 @@ def test_fourier_path_partials_combine():
         parts.append(dm.partial(y))
     ho = O.estimate(means, covs, w, y, 5.0, N, None, "all", 1)
     assert rel_fro(combine_partials_numpy(parts, N), ho) < 1e-6
+
+
+@pytest.mark.parametrize("K,N,blocks,B,n_bits,mean", [
+    (40, 128, None, 333, 1, True),       # 1-D N=128: two waves split the bins; K padded to 48
+    (7, 256, (2, 128), 101, 2, False),   # K < 16: one component block, mostly padding
+    (130, 64, (8, 8), 777, 3, False),    # 2-D radix-8 x radix-8, K = 130 -> 144
+    (33, 256, (4, 64), 64, np.inf, True),
+])
+def test_fourier_mfma_kernel_vs_lds_kernel(K, N, blocks, B, n_bits, mean, monkeypatch):
+    """The MFMA Fourier kernel (qce_fft_mfma.hip, default) against the LDS-tiled FP64 kernel
+    (qce_fft.hip, QCE_FFT_KERNEL=lds) and the oracle, 'all' mode and the K-shard partial."""
+    _gpu_or_skip()
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import _lib, inputs
+    from quantized_channel_estimation_amd.sharding import combine_partials_numpy
+    cov = "circulant" if blocks is None else "block-circulant"
+    means, covs, w = inputs.synthetic_model(K, N, cov_type=cov, seed=K, blocks=blocks)
+    rng = np.random.default_rng(K + N)
+    if mean:
+        means = 0.3 * inputs.crandn(K, N, rng=rng)
+    h, _ = inputs.scm_generate(B, 1, N, rng, n_path=3)
+    qz = (None, None, None)
+    qtype = "uniform"
+    if n_bits not in (1, np.inf):
+        qz = inputs.get_quantizer([5.0], n_bits, qtype)[5.0]
+    y = inputs.get_observation_nbit(h[:, 0, :].astype(complex), 5.0, None, n_bits, qz[0], qz[1], rng=rng)
+    out = {}
+    for kern in ("mfma", "lds"):
+        if kern == "lds":
+            monkeypatch.setenv("QCE_FFT_KERNEL", "lds")
+        dm = _lib.DeviceModel(means, covs, w)
+        dm.prepare(None, 5.0, float(n_bits))
+        assert dm.structure()[2] == 1
+        out[kern] = (dm.estimate(y), combine_partials_numpy([dm.partial(y)], N))
+        dm.close()
+    ho = O.estimate(means, covs, w, y, 5.0, N, None, "all", n_bits, qtype, qz)
+    tol = 1e-9 if n_bits != 1 else 1e-7
+    assert rel_fro(out["mfma"][0], ho) < tol
+    assert rel_fro(out["mfma"][0], out["lds"][0]) < 1e-12
+    assert rel_fro(out["mfma"][1], ho) < 1e-6  # partial acc is fp32
