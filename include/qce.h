@@ -103,6 +103,23 @@ int qce_model_info(qce_model* model, int* K, int* N, int* M, int* device);
  * Environment QCE_FFT=0 keeps every prepare on the dense path. */
 int qce_model_structure(qce_model* model, int* n1, int* n2, int* fourier_active);
 
+/* Observations on the device (model-free): `get_observation_nbit` (utils.py:241-251) with `quant`
+ * (utils.py:189-203):  y = Q(A h + noise_scale * w).
+ * h (B,N) c128; A (M,N) c128 host array or NULL for the identity (then M == N); y_out (B,M) c128.
+ * noise_kind: 0 none (pure quantiser, `quant`), 1 w supplied in `noise` (B,M) c128 — the reference's
+ * crandn draw, result bit-identical to numpy for A = NULL —, 2 generated on the device: circular
+ * CN(0,1) from Philox4x32-10 keyed by `seed`, complex element e of the batch uses counter offset + e.
+ * n_bits: 1 (sign law), +INFINITY (no quantisation), else labels[np.digitize(.)] with thresholds
+ * (n_levels - 1, increasing) and labels (n_levels) host arrays.  h / noise / y_out live where `io` says;
+ * `stream` NULL = the null stream of `device`. */
+int qce_observe(const double* h, int64_t B, int N, const double* A, int M, double noise_scale, int noise_kind,
+                const double* noise, uint64_t seed, uint64_t offset, double n_bits, const double* thresholds,
+                const double* labels, int n_levels, double* y_out, int device, int io, void* stream);
+
+/* out[0] = sum |a_i - b_i|^2 over n complex values (the scripts' MSE numerator, Bussgang_GMM.py:289);
+ * deterministic reduction order.  `out` is host memory for QCE_IO_HOST, device memory otherwise. */
+int qce_sq_error(const double* a, const double* b, int64_t n, double* out, int device, int io, void* stream);
+
 /* Device synchronisation of the model's stream (for timing and for QCE_IO_DEVICE callers). */
 int qce_synchronize(qce_model* model);
 

@@ -5,6 +5,6 @@ The compute path is libqce.so (hand-written HIP for gfx950, include/qce.h) bound
 ctypes; there is no CPU fallback.
 """
 from .gmm import GaussianMixtureCplx, Gmm_nbit, Gmm_quant, mp_gmm  # noqa: F401
-from . import inputs  # noqa: F401
+from . import inputs, observe  # noqa: F401
 
-__all__ = ["Gmm_nbit", "Gmm_quant", "GaussianMixtureCplx", "mp_gmm", "inputs"]
+__all__ = ["Gmm_nbit", "Gmm_quant", "GaussianMixtureCplx", "mp_gmm", "inputs", "observe"]

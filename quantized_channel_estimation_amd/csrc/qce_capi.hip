@@ -946,6 +946,124 @@ int qce_model_structure(qce_model* m, int* n1, int* n2, int* fourier_active) {
   return QCE_OK;
 }
 
+namespace {
+
+// stream-ordered scratch for the model-free entry points (freed on the same stream)
+struct StreamScratch {
+  hipStream_t st;
+  std::vector<void*> ptrs;
+  explicit StreamScratch(hipStream_t s) : st(s) {}
+  hipError_t get(void** p, size_t bytes) {
+    hipError_t e = hipMallocAsync(p, bytes ? bytes : 1, st);
+    if (e == hipSuccess) ptrs.push_back(*p);
+    return e;
+  }
+  ~StreamScratch() {
+    for (void* p : ptrs) (void)hipFreeAsync(p, st);
+  }
+};
+
+}  // namespace
+
+int qce_observe(const double* h, int64_t B, int N, const double* A, int M, double noise_scale, int noise_kind,
+                const double* noise, uint64_t seed, uint64_t offset, double n_bits, const double* thresholds,
+                const double* labels, int n_levels, double* y_out, int device, int io, void* stream) {
+  if (B < 0 || N < 1 || (A && M < 1) || (!A && M != N)) return fail(QCE_EARG, "observe: bad shape");
+  if (noise_kind < 0 || noise_kind > 2 || (noise_kind == 1 && !noise)) return fail(QCE_EARG, "observe: bad noise");
+  if (io != QCE_IO_HOST && io != QCE_IO_DEVICE) return fail(QCE_EARG, "observe: bad io");
+  if (B > 0 && (!h || !y_out)) return fail(QCE_EARG, "observe: null buffer");
+  int kind;
+  if (n_bits == 1.0) kind = 0;
+  else if (isinf(n_bits) && n_bits > 0) kind = 2;
+  else {
+    kind = 1;
+    if (!thresholds || !labels || n_levels < 2 || n_levels > 256)
+      return fail(QCE_EARG, "observe: multi-bit quantisation needs thresholds (L-1) and labels (L), 2 <= L <= 256");
+    for (int i = 1; i < n_levels - 1; ++i)
+      if (!(thresholds[i] >= thresholds[i - 1])) return fail(QCE_EARG, "observe: thresholds must be increasing");
+  }
+  if (B == 0) return QCE_OK;
+  DeviceGuard g(device);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t ny = (size_t)B * M, nh = (size_t)B * N;
+  QceObserveArgs a;
+  a.B = B;
+  a.M = M;
+  a.N = N;
+  a.noise = noise_kind;
+  a.noise_scale = noise_scale;
+  a.seed = seed;
+  a.offset = offset;
+  a.kind = kind;
+  a.nthr = kind == 1 ? n_levels - 1 : 0;
+  {
+    StreamScratch sc(st);
+    void* p;
+    a.A = nullptr;
+    if (A) {
+      HIPCHK(sc.get(&p, sizeof(double2) * (size_t)M * N));
+      HIPCHK(hipMemcpyAsync(p, A, sizeof(double2) * (size_t)M * N, hipMemcpyHostToDevice, st));
+      a.A = (const double2*)p;
+    }
+    a.thr = a.lab = nullptr;
+    if (kind == 1) {
+      HIPCHK(sc.get(&p, sizeof(double) * (size_t)(2 * n_levels - 1)));
+      HIPCHK(hipMemcpyAsync(p, thresholds, sizeof(double) * (n_levels - 1), hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync((double*)p + n_levels - 1, labels, sizeof(double) * n_levels, hipMemcpyHostToDevice, st));
+      a.thr = (const double*)p;
+      a.lab = (const double*)p + n_levels - 1;
+    }
+    if (io == QCE_IO_HOST) {
+      HIPCHK(sc.get(&p, sizeof(double2) * nh));
+      HIPCHK(hipMemcpyAsync(p, h, sizeof(double2) * nh, hipMemcpyHostToDevice, st));
+      a.h = (const double2*)p;
+      a.w = nullptr;
+      if (noise_kind == 1) {
+        HIPCHK(sc.get(&p, sizeof(double2) * ny));
+        HIPCHK(hipMemcpyAsync(p, noise, sizeof(double2) * ny, hipMemcpyHostToDevice, st));
+        a.w = (const double2*)p;
+      }
+      HIPCHK(sc.get(&p, sizeof(double2) * ny));
+      a.y = (double2*)p;
+    } else {
+      a.h = (const double2*)h;
+      a.w = (const double2*)noise;
+      a.y = (double2*)y_out;
+    }
+    HIPCHK(qce_launch_observe(a, st));
+    if (io == QCE_IO_HOST) HIPCHK(hipMemcpyAsync(y_out, a.y, sizeof(double2) * ny, hipMemcpyDeviceToHost, st));
+  }
+  if (io == QCE_IO_HOST) HIPCHK(hipStreamSynchronize(st));
+  return QCE_OK;
+}
+
+int qce_sq_error(const double* a, const double* b, int64_t n, double* out, int device, int io, void* stream) {
+  if (n < 0 || !out || (n > 0 && (!a || !b))) return fail(QCE_EARG, "sq_error: bad arguments");
+  if (io != QCE_IO_HOST && io != QCE_IO_DEVICE) return fail(QCE_EARG, "sq_error: bad io");
+  DeviceGuard g(device);
+  hipStream_t st = (hipStream_t)stream;
+  {
+    StreamScratch sc(st);
+    void *pa, *pb, *part, *po;
+    HIPCHK(sc.get(&part, sizeof(double) * qce_sq_err_scratch()));
+    if (io == QCE_IO_HOST) {
+      HIPCHK(sc.get(&pa, sizeof(double2) * (size_t)n));
+      HIPCHK(sc.get(&pb, sizeof(double2) * (size_t)n));
+      HIPCHK(sc.get(&po, sizeof(double)));
+      HIPCHK(hipMemcpyAsync(pa, a, sizeof(double2) * (size_t)n, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(pb, b, sizeof(double2) * (size_t)n, hipMemcpyHostToDevice, st));
+    } else {
+      pa = (void*)a;
+      pb = (void*)b;
+      po = out;
+    }
+    HIPCHK(qce_launch_sq_err(n, (const double2*)pa, (const double2*)pb, (double*)part, (double*)po, st));
+    if (io == QCE_IO_HOST) HIPCHK(hipMemcpyAsync(out, po, sizeof(double), hipMemcpyDeviceToHost, st));
+  }
+  if (io == QCE_IO_HOST) HIPCHK(hipStreamSynchronize(st));
+  return QCE_OK;
+}
+
 int qce_synchronize(qce_model* m) {
   if (!m) return fail(QCE_EARG, "null model");
   DeviceGuard g(m->device);

@@ -152,3 +152,24 @@ int qce_fft_kpad(int K);
 hipError_t qce_launch_fft_pack(const QceFftEstArgs& a, const double* rinvT, const double2* uT, const double* cprime,
                                const double* wT, const double2* bT, hipStream_t st);
 hipError_t qce_launch_fft_mfma(const QceFftEstArgs& a, int out, hipStream_t st);
+
+// Observation generation / quantisation (qce_observe.hip; utils.py:189-203, :241-251)
+struct QceObserveArgs {
+  long long B;
+  int M, N;
+  const double2* A;  // M x N, nullptr = identity (M == N)
+  const double2* h;  // B x N
+  const double2* w;  // B x M supplied noise (noise == 1)
+  int noise;         // 0 none, 1 supplied, 2 generated (Philox, seed, element offset)
+  double noise_scale;
+  unsigned long long seed, offset;
+  int kind;  // 0: 1 bit, 1: multi-bit (thr / lab), 2: unquantised
+  const double* thr;
+  const double* lab;
+  int nthr;
+  double2* y;  // B x M
+};
+hipError_t qce_launch_observe(const QceObserveArgs& a, hipStream_t st);
+int qce_sq_err_scratch();
+hipError_t qce_launch_sq_err(long long n, const double2* a, const double2* b, double* part, double* out,
+                             hipStream_t st);
