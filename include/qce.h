@@ -120,6 +120,21 @@ int qce_observe(const double* h, int64_t B, int N, const double* A, int M, doubl
  * deterministic reduction order.  `out` is host memory for QCE_IO_HOST, device memory otherwise. */
 int qce_sq_error(const double* a, const double* b, int64_t n, double* out, int device, int io, void* stream);
 
+/* EM training on the device (gmm_cplx_bussgang.py:437-790, `fit_cplx` / `_e_step` / `_m_step`).
+ * E-step: the model must be prepared as the fit's channel-domain model (A = NULL, snr_db = +INFINITY,
+ * n_bits = +INFINITY: Cr = C).  resp_out (B,K) f64 = exp(log_resp) (:612-656, :676);
+ * mean_lse_out[0] = mean_b logsumexp_k lp (the lower bound, :629).  Both where `io` says. */
+int qce_em_estep(qce_model* model, const double* X, int64_t B, double* resp_out, double* mean_lse_out, int io,
+                 void* stream);
+
+/* M-step `estimate_gaussian_parameters` (:698-737): X (B,N) c128, resp (B,K) f64 ->
+ * nk_out (K,) = sum_b resp + 10 eps, means_out (K,N) c128 (zeros when zero_mean), and
+ * diag == 0: covs_out (K,N,N) c128 ('full', :739-765); diag != 0: covs_out (K,N) f64 ('diag', :767-790).
+ * N <= 256.  Buffers where `io` says (model-free; `stream` NULL = the null stream of `device`). */
+int qce_em_mstep(const double* X, int64_t B, int N, int K, const double* resp, double reg_covar, int diag,
+                 int zero_mean, double* nk_out, double* means_out, double* covs_out, int device, int io,
+                 void* stream);
+
 /* Device synchronisation of the model's stream (for timing and for QCE_IO_DEVICE callers). */
 int qce_synchronize(qce_model* model);
 

@@ -42,6 +42,9 @@ SIGNATURES = {
                                    _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double, _vp, _vp, ctypes.c_int, _vp,
                                    ctypes.c_int, ctypes.c_int, _vp]),
     "qce_sq_error": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, ctypes.c_int, ctypes.c_int, _vp]),
+    "qce_em_estep": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp]),
+    "qce_em_mstep": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_double,
+                                    ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, _vp]),
     "qce_model_structure": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                            ctypes.POINTER(ctypes.c_int)]),
 }

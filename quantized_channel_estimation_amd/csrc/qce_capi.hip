@@ -1064,6 +1064,107 @@ int qce_sq_error(const double* a, const double* b, int64_t n, double* out, int d
   return QCE_OK;
 }
 
+int qce_em_estep(qce_model* m, const double* X, int64_t B, double* resp_out, double* mean_lse_out, int io,
+                 void* stream) {
+  int rc = check_model(m, true);
+  if (rc) return rc;
+  if (B < 1 || !X || !resp_out || !mean_lse_out) return fail(QCE_EARG, "em_estep: bad arguments");
+  if (io != QCE_IO_HOST && io != QCE_IO_DEVICE) return fail(QCE_EARG, "em_estep: bad io");
+  DeviceGuard g(m->device);
+  hipStream_t st = pick_stream(m, stream);
+  const double2* dx = nullptr;
+  if ((rc = stage_input(m, X, B, io, st, &dx))) return rc;
+  const size_t BK = (size_t)B * m->K;
+  HIPCHK(m->lp_scr.ensure(BK));
+  double* dlp = m->lp_scr.p;
+  if (m->fft_active) {
+    QceFftEstArgs fa = fft_args(m, dx, B);
+    fa.lp = dlp;
+    HIPCHK(qce_launch_fft_est(fa, 1, st));
+  } else {
+    QceEstArgs a = est_args(m, dx, B);
+    HIPCHK(qce_launch_lp(a, dlp, st));
+  }
+  {
+    StreamScratch sc(st);
+    void *lse, *part, *dresp = resp_out, *dmean = mean_lse_out;
+    HIPCHK(sc.get(&lse, sizeof(double) * (size_t)B));
+    HIPCHK(sc.get(&part, sizeof(double) * qce_mean_scratch()));
+    if (io == QCE_IO_HOST) {
+      HIPCHK(sc.get(&dresp, sizeof(double) * BK));
+      HIPCHK(sc.get(&dmean, sizeof(double)));
+    }
+    HIPCHK(qce_launch_em_resp(B, m->K, dlp, (double*)dresp, (double*)lse, (double*)part, (double*)dmean, st));
+    if (io == QCE_IO_HOST) {
+      HIPCHK(hipMemcpyAsync(resp_out, dresp, sizeof(double) * BK, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(mean_lse_out, dmean, sizeof(double), hipMemcpyDeviceToHost, st));
+    }
+  }
+  if (io == QCE_IO_HOST) HIPCHK(hipStreamSynchronize(st));
+  return QCE_OK;
+}
+
+int qce_em_mstep(const double* X, int64_t B, int N, int K, const double* resp, double reg_covar, int diag,
+                 int zero_mean, double* nk_out, double* means_out, double* covs_out, int device, int io,
+                 void* stream) {
+  if (B < 1 || N < 1 || N > 256 || K < 1 || !X || !resp || !nk_out || !means_out || !covs_out)
+    return fail(QCE_EARG, "em_mstep: bad arguments");
+  if (io != QCE_IO_HOST && io != QCE_IO_DEVICE) return fail(QCE_EARG, "em_mstep: bad io");
+  DeviceGuard g(device);
+  hipStream_t st = (hipStream_t)stream;
+  QceEmArgs a;
+  a.B = B;
+  a.N = N;
+  a.K = K;
+  a.diag = diag ? 1 : 0;
+  a.zero_mean = zero_mean ? 1 : 0;
+  a.reg = reg_covar;
+  a.plan = qce_em_plan(B, N, K, a.diag);
+  const size_t nX = (size_t)B * N, nR = (size_t)B * K, nM = (size_t)K * N;
+  const size_t nC = a.diag ? nM : nM * N;
+  const size_t cov_bytes = a.diag ? sizeof(double) * nC : sizeof(double2) * nC;
+  {
+    StreamScratch sc(st);
+    void* p;
+    HIPCHK(sc.get(&p, sizeof(double) * a.plan.stat_doubles));
+    a.stats = (double*)p;
+    a.part = nullptr;
+    if (!a.diag) {
+      HIPCHK(sc.get(&p, sizeof(double2) * a.plan.part_elems));
+      a.part = (double2*)p;
+    }
+    if (io == QCE_IO_HOST) {
+      HIPCHK(sc.get(&p, sizeof(double2) * nX));
+      HIPCHK(hipMemcpyAsync(p, X, sizeof(double2) * nX, hipMemcpyHostToDevice, st));
+      a.X = (const double2*)p;
+      HIPCHK(sc.get(&p, sizeof(double) * nR));
+      HIPCHK(hipMemcpyAsync(p, resp, sizeof(double) * nR, hipMemcpyHostToDevice, st));
+      a.R = (const double*)p;
+      HIPCHK(sc.get(&p, sizeof(double) * K));
+      a.nk = (double*)p;
+      HIPCHK(sc.get(&p, sizeof(double2) * nM));
+      a.means = (double2*)p;
+      HIPCHK(sc.get(&p, cov_bytes));
+    } else {
+      a.X = (const double2*)X;
+      a.R = resp;
+      a.nk = nk_out;
+      a.means = (double2*)means_out;
+      p = covs_out;
+    }
+    a.covs = a.diag ? nullptr : (double2*)p;
+    a.diag_out = a.diag ? (double*)p : nullptr;
+    HIPCHK(qce_launch_em_mstep(a, st));
+    if (io == QCE_IO_HOST) {
+      HIPCHK(hipMemcpyAsync(nk_out, a.nk, sizeof(double) * K, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(means_out, a.means, sizeof(double2) * nM, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(covs_out, p, cov_bytes, hipMemcpyDeviceToHost, st));
+    }
+  }
+  if (io == QCE_IO_HOST) HIPCHK(hipStreamSynchronize(st));
+  return QCE_OK;
+}
+
 int qce_synchronize(qce_model* m) {
   if (!m) return fail(QCE_EARG, "null model");
   DeviceGuard g(m->device);

@@ -173,3 +173,32 @@ hipError_t qce_launch_observe(const QceObserveArgs& a, hipStream_t st);
 int qce_sq_err_scratch();
 hipError_t qce_launch_sq_err(long long n, const double2* a, const double2* b, double* part, double* out,
                              hipStream_t st);
+
+// EM training (qce_em.hip; gmm_cplx_bussgang.py:612-790)
+struct QceEmPlan {
+  int C = 0;      // stats chunks of 1024 samples
+  int NT = 0;     // 16-wide feature tiles
+  int nblk = 0;   // 64 x 64 output blocks
+  int chunk = 0;  // samples per covariance workgroup
+  int C2 = 0;     // covariance chunks
+  size_t stat_doubles = 0, part_elems = 0;
+};
+QceEmPlan qce_em_plan(long long B, int N, int K, int diag);
+struct QceEmArgs {
+  long long B;
+  int N, K, diag, zero_mean;
+  double reg;
+  QceEmPlan plan;
+  const double2* X;  // B x N
+  const double* R;   // B x K responsibilities
+  double* stats;     // plan.stat_doubles
+  double2* part;     // plan.part_elems
+  double* nk;        // K
+  double2* means;    // K x N
+  double2* covs;     // K x N x N ('full')
+  double* diag_out;  // K x N ('diag')
+};
+hipError_t qce_launch_em_mstep(const QceEmArgs& a, hipStream_t st);
+int qce_mean_scratch();
+hipError_t qce_launch_em_resp(long long B, int K, const double* lp, double* resp, double* lse, double* part,
+                              double* mean_out, hipStream_t st);

@@ -9,8 +9,8 @@ on the GPU; this module only orchestrates and mirrors the reference's state muta
 (``gm.means_``, ``gm.covariances_``, ``gm.precisions_cholesky_``, ``gm.n_features_in_`` become the
 observation-domain model of the last SNR, :262-313).
 
-The EM ``fit`` (training, :96-163, :437-848) is not on the estimate path; models come from a
-reference-fitted object (``from_reference``), from its attributes, or from ``from_params``.
+Models come from the device EM ``fit`` (:96-163, :437-790; ``_em.py``), from a reference-fitted
+object (``from_reference``), or from ``from_params``.
 """
 import copy
 import numbers
@@ -110,10 +110,65 @@ class Gmm_nbit:
         return obj
 
     def fit(self, h, blocks=None, zero_mean=False):
-        """EM training (gmm_cplx_bussgang.py:96-163) is offline and outside the estimate path
-        this package accelerates."""
-        raise NotImplementedError("Gmm_nbit.fit is not provided by the MI355X estimate path; fit with the reference "
-                                  "and adopt the model with Gmm_nbit.from_reference(fitted)")
+        """EM training on the device (gmm_cplx_bussgang.py:96-163).
+
+        'full': EM on h.  'circulant' / 'block-circulant': EM with diagonal covariances on the
+        (block-)DFT of h, then C_k = F^H diag(c_k) F (:104-134).  The Toeplitz variants use the
+        reference's inverse-EM M-step (:792-826), which is not provided: NotImplementedError."""
+        from . import _em
+        self.params["zero_mean"] = bool(zero_mean)
+        h = np.asarray(h)
+        ct = self.gm.covariance_type
+        self._dev = None
+        self._dev_key = None
+        self._state = None
+        if ct == "circulant":
+            self.gm.covariance_type = "diag"
+            N = h.shape[-1]
+            F = np.fft.fft(np.eye(N, dtype=complex)) / np.sqrt(N)
+            self.fit_cplx(np.fft.fft(h, axis=1) / np.sqrt(N))
+            self.fft_covs = self.gm.covariances_
+            self.fft_means = self.gm.means_
+            self._fourier_params(F)
+            self.gm.covariances_ = self.covs_cplx
+        elif ct == "block-circulant":
+            self.gm.covariance_type = "diag"
+            n_1, n_2 = blocks
+            F = np.kron(np.fft.fft(np.eye(n_1)) / np.sqrt(n_1), np.fft.fft(np.eye(n_2)) / np.sqrt(n_2))
+            self.F2 = F
+            self.fit_cplx(np.ascontiguousarray((F @ h.T).T))
+            self._fourier_params(F)  # the reference leaves gm.covariances_ diagonal here (:118-134)
+        elif ct == "full":
+            self.fit_cplx(h)
+            self.means_cplx = self.gm.means_.copy()
+            self.covs_cplx = self.gm.covariances_.copy()
+            self.chol = self.gm.precisions_cholesky_.copy()
+        elif ct in ("toeplitz", "block-toeplitz"):
+            raise NotImplementedError(f"Fitting for covariance_type = {ct} (inverse EM) is not provided on the device")
+        else:
+            raise NotImplementedError(f"Fitting for covariance_type = {ct} is not implemented.")
+        return self
+
+    def _fourier_params(self, F):
+        """Channel-domain model of a diagonal fit in the F basis (:109-117, :127-134)."""
+        from . import _em
+        c = np.asarray(self.gm.covariances_)
+        self.means_cplx = self.gm.means_ @ F.conj()
+        self.covs_cplx = np.einsum("ji,kj,jl->kil", F.conj(), c.astype(complex), F)
+        self.chol = _em.precision_cholesky(self.covs_cplx, device=self.device)
+        self.gm.covariance_type = "full"
+        self.gm.means_ = self.means_cplx
+        self.gm.precisions_cholesky_ = self.chol
+
+    def fit_cplx(self, X, y=None):
+        """gmm_cplx_bussgang.py:437-460."""
+        self.fit_predict(X, y)
+        return self
+
+    def fit_predict(self, X, y=None):
+        """gmm_cplx_bussgang.py:462-536: EM on the device, returns the component labels of X."""
+        from . import _em
+        return _em.fit_predict(self, X)
 
     # ------------------------------------------------------------------ pickling (pool.starmap, :282-287)
     def __getstate__(self):
