@@ -60,6 +60,9 @@ int qce_device_count(int* count);
 int qce_model_create(int K, int N, const double* means_cplx, const double* covs_cplx, const double* weights,
                      int device, qce_model** out);
 int qce_model_destroy(qce_model* model);
+/* Replace the parameters of a model in place (same K, N; e.g. between EM iterations): re-uploads
+ * means / covariances / weights, re-detects the structure and drops the prepared state. */
+int qce_model_set_params(qce_model* model, const double* means_cplx, const double* covs_cplx, const double* weights);
 
 /* Per-SNR precompute: `_prepare_for_prediction` (gmm_cplx_bussgang.py:246-328).
  * A: (M,N) c128 observation matrix, or NULL for the identity (estimate_from_y :191-192).

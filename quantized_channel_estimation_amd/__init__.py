@@ -5,6 +5,7 @@ The compute path is libqce.so (hand-written HIP for gfx950, include/qce.h) bound
 ctypes; there is no CPU fallback.
 """
 from .gmm import GaussianMixtureCplx, Gmm_nbit, Gmm_quant, mp_gmm  # noqa: F401
+from .mofa import Mofa  # noqa: F401
 from . import inputs, observe  # noqa: F401
 
-__all__ = ["Gmm_nbit", "Gmm_quant", "GaussianMixtureCplx", "mp_gmm", "inputs", "observe"]
+__all__ = ["Gmm_nbit", "Gmm_quant", "GaussianMixtureCplx", "mp_gmm", "Mofa", "inputs", "observe"]

@@ -58,6 +58,7 @@ class DeviceEM:
         self.mu = torch.empty((self.K, self.N), dtype=torch.complex128, device=self.dev)
         shape = (self.K, self.N) if self.diag else (self.K, self.N, self.N)
         self.cov = torch.empty(shape, dtype=torch.float64 if self.diag else torch.complex128, device=self.dev)
+        self._dm = None
 
     def _stream(self):
         return _torch().cuda.current_stream(self.dev).cuda_stream
@@ -78,15 +79,21 @@ class DeviceEM:
 
     def estep(self, means, covs_full, weights):
         """_e_step (:612-630): responsibilities into self.R, returns mean log p(x)."""
-        dm = _lib.DeviceModel(means, covs_full, weights, device=self.device)
-        try:
-            dm.prepare(None, float("inf"), float("inf"), stream=self._stream())
-            _lib.check(_lib.load().qce_em_estep(dm.handle, _lib.ptr(self.X), self.B, _lib.ptr(self.R),
-                                                _lib.ptr(self.lse), _lib.IO_DEVICE, self._stream()))
-            return float(self.lse.cpu().numpy()[0])
-        finally:
-            _torch().cuda.synchronize(self.dev)
-            dm.close()
+        _torch().cuda.current_stream(self.dev).synchronize()  # R / X consumers done before tables change
+        if self._dm is None:
+            self._dm = _lib.DeviceModel(means, covs_full, weights, device=self.device)
+        else:
+            self._dm.set_params(means, covs_full, weights)
+        self._dm.prepare(None, float("inf"), float("inf"), stream=self._stream())
+        _lib.check(_lib.load().qce_em_estep(self._dm.handle, _lib.ptr(self.X), self.B, _lib.ptr(self.R),
+                                            _lib.ptr(self.lse), _lib.IO_DEVICE, self._stream()))
+        return float(self.lse.cpu().numpy()[0])
+
+    def close(self):
+        if self._dm is not None:
+            _torch().cuda.current_stream(self.dev).synchronize()
+            self._dm.close()
+            self._dm = None
 
     def labels(self):
         return self.R.argmax(dim=1).cpu().numpy()
@@ -167,7 +174,9 @@ def fit_predict(obj, X):
     gm.n_iter_ = best_n_iter
     gm.lower_bound_ = max_lower_bound
     em.estep(gm.means_, covs_full, gm.weights_)  # final e-step (:532-534)
-    return em.labels()
+    labels = em.labels()
+    em.close()
+    return labels
 
 
 def _initialize_parameters(obj, em, X, random_state):

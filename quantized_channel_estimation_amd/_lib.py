@@ -29,6 +29,7 @@ SIGNATURES = {
     "qce_model_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, ctypes.c_int,
                                         ctypes.POINTER(_vp)]),
     "qce_model_destroy": (ctypes.c_int, [_vp]),
+    "qce_model_set_params": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
     "qce_prepare": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int, _vp, _vp,
                                    ctypes.c_int, _vp]),
     "qce_estimate": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, _vp, ctypes.c_int, _vp]),
@@ -128,6 +129,17 @@ class DeviceModel:
     @property
     def handle(self):
         return self._h
+
+    def set_params(self, means_cplx, covs_cplx, weights):
+        """Same K, N; new parameters (prepared state dropped)."""
+        covs = np.ascontiguousarray(covs_cplx, dtype=np.complex128)
+        if covs.shape != (self.K, self.N, self.N):
+            raise ValueError(f"covariances must be ({self.K}, {self.N}, {self.N})")
+        means = None if means_cplx is None else np.ascontiguousarray(means_cplx, dtype=np.complex128).reshape(
+            self.K, self.N)
+        w = np.ascontiguousarray(weights, dtype=np.float64).reshape(self.K)
+        check(load().qce_model_set_params(self._h, ptr(means), ptr(covs), ptr(w)))
+        self.M = 0
 
     def close(self):
         if getattr(self, "_h", None):

@@ -416,6 +416,33 @@ int qce_model_create(int K, int N, const double* means_cplx, const double* covs_
   return QCE_OK;
 }
 
+int qce_model_set_params(qce_model* m, const double* means_cplx, const double* covs_cplx, const double* weights) {
+  if (!m || !covs_cplx || !weights) return fail(QCE_EARG, "null argument");
+  DeviceGuard g(m->device);
+  const int K = m->K, N = m->N;
+  HIPCHK(hipStreamSynchronize(m->stream));
+  m->weights.assign(weights, weights + K);
+  std::vector<double> logw(K);
+  for (int k = 0; k < K; ++k) logw[k] = log(weights[k]);
+  std::vector<double> mz((size_t)2 * K * N, 0.0);
+  m->has_mean = 0;
+  if (means_cplx) {
+    memcpy(mz.data(), means_cplx, sizeof(double) * 2 * (size_t)K * N);
+    for (double v : mz)
+      if (v != 0.0) {
+        m->has_mean = 1;
+        break;
+      }
+  }
+  HIPCHK(hipMemcpyAsync(m->means.p, mz.data(), sizeof(double2) * (size_t)K * N, hipMemcpyHostToDevice, m->stream));
+  HIPCHK(hipMemcpyAsync(m->covs.p, covs_cplx, sizeof(double2) * (size_t)K * N * N, hipMemcpyHostToDevice, m->stream));
+  HIPCHK(hipMemcpyAsync(m->logw.p, logw.data(), sizeof(double) * K, hipMemcpyHostToDevice, m->stream));
+  HIPCHK(hipStreamSynchronize(m->stream));
+  m->prepared = 0;
+  HIPCHK(detect_structure(m));
+  return QCE_OK;
+}
+
 int qce_model_destroy(qce_model* m) {
   if (!m) return QCE_OK;
   DeviceGuard g(m->device);

@@ -20,30 +20,65 @@ namespace {
 constexpr double EPS10 = 10.0 * 2.220446049250313e-16;  // 10 * np.finfo(float64).eps (:721)
 constexpr int STAT_CHUNK = 1024;
 
-// per (component, sample chunk): sum r, sum r x (N), sum r |x|^2 (N)
+// per (block of STAT_KB components, sample chunk): sum r, sum r x (N), sum r |x|^2 (N).
+// Thread = (sample group g, feature f); each x is loaded once for STAT_KB components; the G group
+// partials are added through LDS in a fixed order.
+constexpr int STAT_KB = 8;
+
+template <int NPAD>
 __global__ __launch_bounds__(256) void k_em_stats(long long B, int N, int K, const double2* __restrict__ X,
                                                   const double* __restrict__ R, double* __restrict__ pnk,
                                                   double2* __restrict__ psx, double* __restrict__ psxx) {
-  const int k = blockIdx.x, c = blockIdx.y, t = threadIdx.x;
+  constexpr int G = 256 / NPAD;
+  const int k0 = blockIdx.x * STAT_KB, c = blockIdx.y;
+  const int f = threadIdx.x % NPAD, g = threadIdx.x / NPAD;
+  const int nkb = K - k0 < STAT_KB ? K - k0 : STAT_KB;
   const long long b0 = (long long)c * STAT_CHUNK;
   const long long b1 = b0 + STAT_CHUNK < B ? b0 + STAT_CHUNK : B;
-  double nk = 0.0, sxx = 0.0;
-  double2 sx = make_double2(0.0, 0.0);
-  for (long long b = b0; b < b1; ++b) {
-    const double r = R[b * K + k];
-    nk += r;
-    if (t < N) {
-      const double2 x = X[b * N + t];
-      sx.x += r * x.x;
-      sx.y += r * x.y;
-      sxx += r * (x.x * x.x + x.y * x.y);
+  double nk[STAT_KB], sr[STAT_KB], si[STAT_KB], sxx[STAT_KB];
+#pragma unroll
+  for (int j = 0; j < STAT_KB; ++j) nk[j] = sr[j] = si[j] = sxx[j] = 0.0;
+  for (long long b = b0 + g; b < b1; b += G) {
+    const double2 x = f < N ? X[b * N + f] : make_double2(0.0, 0.0);
+    const double xx = x.x * x.x + x.y * x.y;
+    const double* rb = R + b * K + k0;
+#pragma unroll
+    for (int j = 0; j < STAT_KB; ++j) {
+      const double r = j < nkb ? rb[j] : 0.0;
+      nk[j] += r;
+      sr[j] += r * x.x;
+      si[j] += r * x.y;
+      sxx[j] += r * xx;
     }
   }
-  const long long o = (long long)c * K + k;
-  if (t == 0) pnk[o] = nk;
-  if (t < N) {
-    psx[o * N + t] = sx;
-    psxx[o * N + t] = sxx;
+  __shared__ double red[G > 1 ? G - 1 : 1][STAT_KB][4][NPAD];
+  if (G > 1 && g > 0) {
+#pragma unroll
+    for (int j = 0; j < STAT_KB; ++j) {
+      red[g - 1][j][0][f] = nk[j];
+      red[g - 1][j][1][f] = sr[j];
+      red[g - 1][j][2][f] = si[j];
+      red[g - 1][j][3][f] = sxx[j];
+    }
+  }
+  __syncthreads();
+  if (g != 0) return;
+  for (int q = 0; q < G - 1; ++q) {
+#pragma unroll
+    for (int j = 0; j < STAT_KB; ++j) {
+      nk[j] += red[q][j][0][f];
+      sr[j] += red[q][j][1][f];
+      si[j] += red[q][j][2][f];
+      sxx[j] += red[q][j][3][f];
+    }
+  }
+  for (int j = 0; j < nkb; ++j) {
+    const long long o = (long long)c * K + k0 + j;
+    if (f == 0) pnk[o] = nk[j];
+    if (f < N) {
+      psx[o * N + f] = make_double2(sr[j], si[j]);
+      psxx[o * N + f] = sxx[j];
+    }
   }
 }
 
@@ -215,7 +250,10 @@ hipError_t qce_launch_em_mstep(const QceEmArgs& a, hipStream_t st) {
   double* pnk = a.stats;
   double2* psx = reinterpret_cast<double2*>(a.stats + (size_t)p.C * K);
   double* psxx = a.stats + (size_t)p.C * K * (1 + 2 * (size_t)N);
-  hipLaunchKernelGGL(k_em_stats, dim3(K, p.C), dim3(256), 0, st, a.B, N, K, a.X, a.R, pnk, psx, psxx);
+  const dim3 sg((K + STAT_KB - 1) / STAT_KB, p.C);
+  if (N <= 64) hipLaunchKernelGGL(k_em_stats<64>, sg, dim3(256), 0, st, a.B, N, K, a.X, a.R, pnk, psx, psxx);
+  else if (N <= 128) hipLaunchKernelGGL(k_em_stats<128>, sg, dim3(256), 0, st, a.B, N, K, a.X, a.R, pnk, psx, psxx);
+  else hipLaunchKernelGGL(k_em_stats<256>, sg, dim3(256), 0, st, a.B, N, K, a.X, a.R, pnk, psx, psxx);
   hipLaunchKernelGGL(k_em_means, dim3(K), dim3(256), 0, st, p.C, N, K, a.zero_mean, a.diag, a.reg, pnk, psx, psxx,
                      a.nk, a.means, a.diag_out);
   if (!a.diag) {

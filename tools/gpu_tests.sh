@@ -1,15 +1,7 @@
 #!/bin/bash
-# GPU parity tests only (optionally a -k expression), one process, per-test timeout.
+# Whole GPU test suite, one process.
 set -o pipefail
-R=${GRAFT_REPO_ROOT:-$(pwd)}
-cd $R
-mkdir -p gpurun_out
-K=${1:-}
-if [ -n "$K" ]; then
-  timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "$K" > gpurun_out/pytest_sel.log 2>&1
-else
-  timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_sel.log 2>&1
-fi
-rc=$?
-grep -E "PASSED|FAILED|ERROR|passed|failed|Error|assert" gpurun_out/pytest_sel.log | tail -40
-exit $rc
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/tests; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; grep -E "FAILED|ERROR|passed|failed|Error" $O/pytest.log | tail -30; exit $rc
