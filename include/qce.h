@@ -46,6 +46,11 @@ typedef struct qce_model qce_model;
 #define QCE_QUANT_LLOYD 1
 #define QCE_QUANT_OTHER 2 /* any other string: the reference leaves the Bussgang gain at 0 */
 
+/* model options (qce_model_set_option) */
+#define QCE_OPT_BETA_FIRST 1 /* multi-bit Cr = g_0^2 Cy + (1 - g_0^2) diag(Cy) with the first Bussgang gain
+                                (estimators/blmmse.py:53, :86) instead of clip(mean gain, 0, 1)
+                                (gmm_cplx_bussgang.py:304-307); value != 0 enables */
+
 #define QCE_IO_HOST 0
 #define QCE_IO_DEVICE 1
 
@@ -137,6 +142,15 @@ int qce_em_estep(qce_model* model, const double* X, int64_t B, double* resp_out,
 int qce_em_mstep(const double* X, int64_t B, int N, int K, const double* resp, double reg_covar, int diag,
                  int zero_mean, double* nk_out, double* means_out, double* covs_out, int device, int io,
                  void* stream);
+
+/* Set a model option (QCE_OPT_*); drops the prepared state. */
+int qce_model_set_option(qce_model* model, int option, double value);
+
+/* Per-sample filters: h_b = W_c y_b + b_c with c = comp[b] (int64, B entries, NULL: c = b, B <= K).
+ * The genie Bussgang-LMMSE (estimators/blmmse.py:20-62) is a model with one component per sample
+ * (C_b = toeplitz(t_b)^T) estimated this way.  y / comp / h_out where `io` says. */
+int qce_estimate_assigned(qce_model* model, const double* y, int64_t B, const int64_t* comp, double* h_out, int io,
+                          void* stream);
 
 /* Device synchronisation of the model's stream (for timing and for QCE_IO_DEVICE callers). */
 int qce_synchronize(qce_model* model);

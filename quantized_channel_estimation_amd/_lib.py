@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("QCE_LIB") or os.path.join(_PKG, "libqce.so")  # QCE_L
 
 QCE_OK, QCE_EARG, QCE_ECHOL, QCE_ENOTIMPL, QCE_EHIP, QCE_ESTATE = range(6)
 MODE_ALL, MODE_TOPN, MODE_CUMP = 0, 1, 2
+OPT_BETA_FIRST = 1
 QUANT_UNIFORM, QUANT_LLOYD, QUANT_OTHER = 0, 1, 2
 IO_HOST, IO_DEVICE = 0, 1
 
@@ -30,6 +31,8 @@ SIGNATURES = {
                                         ctypes.POINTER(_vp)]),
     "qce_model_destroy": (ctypes.c_int, [_vp]),
     "qce_model_set_params": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
+    "qce_model_set_option": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double]),
+    "qce_estimate_assigned": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp]),
     "qce_prepare": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int, _vp, _vp,
                                    ctypes.c_int, _vp]),
     "qce_estimate": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, _vp, ctypes.c_int, _vp]),
@@ -214,6 +217,21 @@ class DeviceModel:
             acc_out = torch.empty((B, 2 * self.N), dtype=torch.float32, device=dev) if acc_out is None else acc_out
         check(load().qce_estimate_partial(self._h, ptr(y), int(B), ptr(m_out), ptr(s_out), ptr(acc_out), io, stream))
         return m_out, s_out, acc_out
+
+    def set_option(self, option, value):
+        check(load().qce_model_set_option(self._h, int(option), float(value)))
+        self.M = 0
+
+    def estimate_assigned(self, y, comp=None):
+        """h_b = W_c y_b + b_c, c = comp[b] (None: c = b); host numpy I/O."""
+        y = np.ascontiguousarray(y, dtype=np.complex128)
+        B = y.shape[0]
+        if y.ndim != 2 or y.shape[1] != self.M:
+            raise ValueError(f"y must be (B, {self.M})")
+        c = None if comp is None else np.ascontiguousarray(comp, dtype=np.int64).reshape(B)
+        out = np.empty((B, self.N), dtype=np.complex128)
+        check(load().qce_estimate_assigned(self._h, ptr(y), int(B), ptr(c), ptr(out), IO_HOST, None))
+        return out
 
     def tables(self):
         K, M, N = self.K, self.M, self.N

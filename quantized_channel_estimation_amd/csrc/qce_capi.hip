@@ -62,6 +62,7 @@ int pad_dim(int v) {
 
 struct qce_model {
   int K = 0, N = 0, device = 0;
+  int beta_first = 0;  // QCE_OPT_BETA_FIRST: multi-bit Cr mixes with the first gain (blmmse.py:53, :86)
   hipStream_t stream = nullptr;
   int has_mean = 0;
   std::vector<double> weights;
@@ -547,7 +548,7 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
                        thresholds && kind == 1 ? thresholds + (n_levels > 0 ? n_levels - 1 : 0) : nullptr);
     m->last.lab.assign(labels && kind == 1 ? labels : nullptr, labels && kind == 1 ? labels + n_levels : nullptr);
   }
-  if (allow_fft && idA && m->fft_n1 > 0 && fft_enabled()) {
+  if (allow_fft && idA && m->fft_n1 > 0 && fft_enabled() && !m->beta_first) {
     // Fourier-domain prepare (qce_fft.hip): per-bin tables only
     HIPCHK(m->f_rinvT.ensure((size_t)N * K));
     HIPCHK(m->f_uT.ensure((size_t)N * K));
@@ -695,6 +696,7 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
   p.kind = kind;
   p.n_bits = nb;
   p.quant_kind = quant_kind;
+  p.beta_first = m->beta_first;
   p.sigma2 = pow(10.0, -snr_db / 10.0);
   p.delta = delta;
   p.thr = m->thr.p;
@@ -1187,6 +1189,52 @@ int qce_em_mstep(const double* X, int64_t B, int N, int K, const double* resp, d
       HIPCHK(hipMemcpyAsync(means_out, a.means, sizeof(double2) * nM, hipMemcpyDeviceToHost, st));
       HIPCHK(hipMemcpyAsync(covs_out, p, cov_bytes, hipMemcpyDeviceToHost, st));
     }
+  }
+  if (io == QCE_IO_HOST) HIPCHK(hipStreamSynchronize(st));
+  return QCE_OK;
+}
+
+int qce_model_set_option(qce_model* m, int option, double value) {
+  if (!m) return fail(QCE_EARG, "null model");
+  if (option == QCE_OPT_BETA_FIRST) {
+    m->beta_first = value != 0.0;
+    m->prepared = 0;
+    return QCE_OK;
+  }
+  return fail(QCE_EARG, "unknown option");
+}
+
+int qce_estimate_assigned(qce_model* m, const double* y, int64_t B, const int64_t* comp, double* h_out, int io,
+                          void* stream) {
+  int rc = check_model(m, true);
+  if (rc) return rc;
+  if (B < 0 || (B > 0 && (!y || !h_out))) return fail(QCE_EARG, "bad arguments");
+  if (!comp && B > m->K) return fail(QCE_EARG, "without comp, sample b uses component b: B <= K");
+  if (B == 0) return QCE_OK;
+  if ((rc = ensure_dense(m))) return rc;
+  DeviceGuard g(m->device);
+  hipStream_t st = pick_stream(m, stream);
+  const double2* dy = nullptr;
+  if ((rc = stage_input(m, y, B, io, st, &dy))) return rc;
+  {
+    StreamScratch sc(st);
+    void* p;
+    const long long* dc = reinterpret_cast<const long long*>(comp);
+    double2* dh = reinterpret_cast<double2*>(h_out);
+    if (comp && io == QCE_IO_HOST) {
+      for (int64_t b = 0; b < B; ++b)
+        if (comp[b] < 0 || comp[b] >= m->K) return fail(QCE_EARG, "component index out of range");
+      HIPCHK(sc.get(&p, sizeof(long long) * (size_t)B));
+      HIPCHK(hipMemcpyAsync(p, comp, sizeof(long long) * (size_t)B, hipMemcpyHostToDevice, st));
+      dc = (const long long*)p;
+    }
+    if (io == QCE_IO_HOST) {
+      HIPCHK(sc.get(&p, sizeof(double2) * (size_t)B * m->N));
+      dh = (double2*)p;
+    }
+    HIPCHK(qce_launch_est_assigned(B, m->N, m->M, m->K, dy, dc, m->W.p, m->bvec.p, dh, st));
+    if (io == QCE_IO_HOST)
+      HIPCHK(hipMemcpyAsync(h_out, dh, sizeof(double2) * (size_t)B * m->N, hipMemcpyDeviceToHost, st));
   }
   if (io == QCE_IO_HOST) HIPCHK(hipStreamSynchronize(st));
   return QCE_OK;

@@ -1,0 +1,43 @@
+// Per-sample ("assigned component") LMMSE: h_b = W_c y_b + b_c, c = comp[b] (or b).  Serves the genie
+// Bussgang-LMMSE baseline (estimators/blmmse.py:20-62 estimate_genie: one covariance per sample, so
+// the model holds one component per sample and each sample uses its own filter) and any caller
+// that has already chosen the component.  FP64, like the reference.
+//
+// One wave per sample, lane = output row(s); y_b is broadcast from LDS; W_c rows are read with
+// lane-strided addresses whose cache lines are consumed over consecutive m.  HBM-bound: the
+// filter (16 N M bytes) dominates per sample.
+#include "qce_common.h"
+#include "qce_kernels.h"
+
+namespace {
+
+__global__ __launch_bounds__(256) void k_est_assigned(long long B, int N, int M, const double2* __restrict__ y,
+                                                      const long long* __restrict__ comp,
+                                                      const double2* __restrict__ W,
+                                                      const double2* __restrict__ bvec, double2* __restrict__ h) {
+  __shared__ double2 ys[4][256];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long b = (long long)blockIdx.x * 4 + w;
+  const bool live = b < B;
+  if (live)
+    for (int m = lane; m < M; m += 64) ys[w][m] = y[b * M + m];
+  __syncthreads();
+  if (!live) return;
+  const long long c = comp ? comp[b] : b;
+  const double2* Wc = W + c * (long long)N * M;
+  for (int n = lane; n < N; n += 64) {
+    const double2* row = Wc + (long long)n * M;
+    double2 acc = bvec[c * N + n];
+    for (int m = 0; m < M; ++m) acc = cfma(row[m], ys[w][m], acc);
+    h[b * N + n] = acc;
+  }
+}
+
+}  // namespace
+
+hipError_t qce_launch_est_assigned(long long B, int N, int M, int K, const double2* y, const long long* comp,
+                                   const double2* W, const double2* bvec, double2* h, hipStream_t st) {
+  (void)K;
+  hipLaunchKernelGGL(k_est_assigned, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, N, M, y, comp, W, bvec, h);
+  return hipGetLastError();
+}

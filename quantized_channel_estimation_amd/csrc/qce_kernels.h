@@ -7,6 +7,7 @@ struct QcePrepareArgs {
   int kind;        // 0: 1 bit, 1: multi-bit, 2: n_bits = inf
   int n_bits;      // multi-bit only
   int quant_kind;  // 0 uniform, 1 lloyd, 2 other (zero gain)
+  int beta_first;  // multi-bit Cr: beta = gain[0] (blmmse.py) instead of clip(mean gain, 0, 1)
   double sigma2, delta;
   const double* thr;  // device, 2^b - 1 entries
   const double* lab;  // device, 2^b entries
@@ -202,3 +203,7 @@ hipError_t qce_launch_em_mstep(const QceEmArgs& a, hipStream_t st);
 int qce_mean_scratch();
 hipError_t qce_launch_em_resp(long long B, int K, const double* lp, double* resp, double* lse, double* part,
                               double* mean_out, hipStream_t st);
+
+// h_b = W_c y_b + b_c with c = comp[b] (comp == nullptr: c = b) — per-sample ("genie") filters
+hipError_t qce_launch_est_assigned(long long B, int N, int M, int K, const double2* y, const long long* comp,
+                                   const double2* W, const double2* bvec, double2* h, hipStream_t st);

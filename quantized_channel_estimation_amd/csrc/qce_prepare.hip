@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void k_gain_cr(int M, int N, const double2* __
                                                  const double2* __restrict__ means, double2* __restrict__ means_y,
                                                  double2* __restrict__ Aeff, int kind, int n_bits, int quant_kind,
                                                  double delta, const double* __restrict__ thr,
-                                                 const double* __restrict__ lab) {
+                                                 const double* __restrict__ lab, int beta_first) {
   const int k = blockIdx.x, tid = threadIdx.x;
   const double2* cy = Cy + (long long)k * M * M;
   double2* cr = Cr + (long long)k * M * M;
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256) void k_gain_cr(int M, int N, const double2* __
     double s = 0.0;
     for (int i = 0; i < M; ++i) s += g[i];
     double beta = s / M;
-    s_beta = beta < 0.0 ? 0.0 : (beta > 1.0 ? 1.0 : beta);
+    s_beta = beta_first ? g[0] : (beta < 0.0 ? 0.0 : (beta > 1.0 ? 1.0 : beta));
   }
   __syncthreads();
   const double beta2 = s_beta * s_beta;
@@ -488,7 +488,7 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(k_gain_cr, dim3(K), dim3(256), 0, st, M, N, p.Cy, p.Cr, p.gain, p.A, p.means, p.means_y, p.Aeff,
-                     p.kind, p.n_bits, p.quant_kind, p.delta, p.thr, p.lab);
+                     p.kind, p.n_bits, p.quant_kind, p.delta, p.thr, p.lab, p.beta_first);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (M <= 64) {
     hipLaunchKernelGGL(k_chol_inv_lds, dim3(K), dim3(256), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);

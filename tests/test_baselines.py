@@ -1,0 +1,64 @@
+"""Global / genie Bussgang-LMMSE baselines (estimators/blmmse.py:20-97).
+
+CPU: the oracle restatement and the Toeplitz construction against the reference's own outputs in
+tests/golden/baselines.npz (make_golden_baselines.py).  GPU: quantized_channel_estimation_amd.baselines
+through libqce.so (K=1 model for the global filter; one component per sample + qce_estimate_assigned for
+the genie) against the same vectors, 1e-5 relative Frobenius (FP64 path: measured ~1e-12)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, rel_fro
+
+
+@pytest.fixture(scope="module")
+def bl():
+    return dict(np.load(os.path.join(GOLDEN, "baselines.npz"), allow_pickle=False))
+
+
+def _case(bl, tag):
+    p = tag + "__"
+    nb = float(bl[p + "n_bits"])
+    A = bl[p + "A"]
+    quantizer = (bl[p + "thr"], bl[p + "lab"], None) if (p + "thr") in bl else (None, None, None)
+    return (bl[p + "y"], float(bl[p + "snr"]), (np.inf if np.isinf(nb) else int(nb)), str(bl[p + "qtype"]),
+            quantizer, None if A.size == 0 else A)
+
+
+TAGS = ["b1", "b2u", "b3l", "inf", "b1_A2", "b2u_A2"]
+
+
+def test_toeplitz_covs_match_scipy(bl):
+    from scipy.linalg import toeplitz
+    from quantized_channel_estimation_amd.baselines import _toeplitz_covs
+    t = bl["t"][:5]
+    C = _toeplitz_covs(t)
+    for b in range(5):
+        assert np.array_equal(C[b], toeplitz(t[b]).T)
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_oracle_blmmse_matches_reference(bl, tag):
+    from scipy.linalg import toeplitz
+    from oracle import qce_oracle as O
+    y, snr, nb, qt, quantizer, A = _case(bl, tag)
+    N = bl["C"].shape[0]
+    Ae = np.eye(N) if A is None else A
+    W = O.blmmse_filter(bl["C"], Ae, snr, nb, qt, quantizer)
+    assert rel_fro(y @ W.T, bl[tag + "__h_global"]) < 1e-9
+    hg = np.stack([O.blmmse_filter(toeplitz(bl["t"][b]).T, Ae, snr, nb, qt, quantizer) @ y[b]
+                   for b in range(y.shape[0])])
+    assert rel_fro(hg, bl[tag + "__h_genie"]) < 1e-9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", TAGS)
+def test_gpu_blmmse_matches_reference(bl, tag):
+    from quantized_channel_estimation_amd.baselines import BLMMSE, mp_eval
+    y, snr, nb, qt, quantizer, A = _case(bl, tag)
+    est = BLMMSE(snr, chunk=50)  # several chunks
+    hg = est.estimate_global(y, bl["C"], A, nb, qt, quantizer)
+    assert rel_fro(hg, bl[tag + "__h_global"]) < 1e-5, tag
+    hq = mp_eval(est, y, bl["t"], None, True, A, nb, qt, quantizer)
+    assert rel_fro(hq, bl[tag + "__h_genie"]) < 1e-5, tag
