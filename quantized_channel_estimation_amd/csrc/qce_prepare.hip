@@ -277,14 +277,18 @@ __global__ __launch_bounds__(256) void k_chol_inv(int M, double2* __restrict__ L
 }
 
 // Same factorisation with the matrix and its inverse resident in LDS (M <= 64: 2 x 64 KB), one
-// workgroup per component; the right-looking updates then cost LDS latency, not L2 round trips.
+// workgroup per component.  Scaling is deferred so every step is ONE barrier phase:
+//   factor  step j:  a_rc -= a_rj conj(a_cj) / a_jj   (r >= c > j; column j and a_jj are final)
+//           afterwards L_ij = a_ij / sqrt(a_jj)
+//   inverse step k:  X~_ic -= a_ik / a_kk * X~_kc      (i > k, c <= k; row k of X~ is final)
+//           afterwards Linv_ic = X~_ic / sqrt(a_ii)
+// (reads and writes of a step touch disjoint entries, so no second barrier is needed).
 __global__ __launch_bounds__(256) void k_chol_inv_lds(int M, const double2* __restrict__ Cr,
                                                       double2* __restrict__ Linv, const double* __restrict__ logw,
                                                       double* __restrict__ cconst, int* __restrict__ status) {
   __shared__ double2 a[64 * 64];
   __shared__ double2 x[64 * 64];
-  __shared__ double s_piv;
-  __shared__ int s_bad;
+  __shared__ double piv[64];
   const int k = blockIdx.x, tid = threadIdx.x;
   const double2* src = Cr + (long long)k * M * M;
   for (int e = tid; e < M * M; e += 256) {
@@ -292,55 +296,54 @@ __global__ __launch_bounds__(256) void k_chol_inv_lds(int M, const double2* __re
     a[r * 64 + c] = src[e];
     x[r * 64 + c] = make_double2(r == c ? 1.0 : 0.0, 0.0);
   }
-  if (tid == 0) s_bad = 0;
   __syncthreads();
+  bool bad = false;
   for (int j = 0; j < M; ++j) {
-    if (tid == 0) {
-      double ajj = a[j * 64 + j].x;
-      if (!(ajj > 0.0)) s_bad = 1;
-      ajj = sqrt(ajj);
-      a[j * 64 + j] = make_double2(ajj, 0.0);
-      s_piv = ajj;
+    const double ajj = a[j * 64 + j].x;  // final: updated by step j - 1 before the barrier
+    if (!(ajj > 0.0)) {                  // same value in every thread: uniform exit
+      bad = true;
+      break;
     }
-    __syncthreads();
-    if (s_bad) break;
-    const double piv = s_piv;
-    for (int i = j + 1 + tid; i < M; i += 256) {
-      const double2 v = a[i * 64 + j];
-      a[i * 64 + j] = make_double2(v.x / piv, v.y / piv);
-    }
-    __syncthreads();
+    const double inv = 1.0 / ajj;
     const int n = M - j - 1;
-    for (int t = tid; t < n * n; t += 256) {
-      const int r = j + 1 + t / n, c = j + 1 + t % n;
-      if (c > r) continue;
-      a[r * 64 + c] = csub(a[r * 64 + c], cmulc(a[r * 64 + j], a[c * 64 + j]));
+    const int tri = n * (n + 1) / 2;
+    for (int t = tid; t < tri; t += 256) {
+      // t -> (r, c) with r >= c in the trailing block, row-major over the lower triangle
+      int rr = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+      if ((rr + 1) * (rr + 2) / 2 <= t) ++rr;
+      if (rr * (rr + 1) / 2 > t) --rr;
+      const int cc = t - rr * (rr + 1) / 2;
+      const int r = j + 1 + rr, c = j + 1 + cc;
+      const double2 arj = a[r * 64 + j], acj = a[c * 64 + j];
+      const double2 pr = cmulc(arj, acj);
+      a[r * 64 + c] = csub(a[r * 64 + c], make_double2(pr.x * inv, pr.y * inv));
     }
     __syncthreads();
   }
-  if (s_bad) {
+  if (bad) {
     if (tid == 0) status[k] = 1;
     return;
   }
+  for (int i = tid; i < M; i += 256) piv[i] = sqrt(a[i * 64 + i].x);
   for (int kk = 0; kk < M; ++kk) {
-    const double d = a[kk * 64 + kk].x;
-    for (int c = tid; c <= kk; c += 256) {
-      const double2 v = x[kk * 64 + c];
-      x[kk * 64 + c] = make_double2(v.x / d, v.y / d);
-    }
-    __syncthreads();
+    const double inv = 1.0 / a[kk * 64 + kk].x;
     const int nr = M - kk - 1, nc = kk + 1;
     for (int t = tid; t < nr * nc; t += 256) {
       const int i = kk + 1 + t / nc, c = t % nc;
-      x[i * 64 + c] = csub(x[i * 64 + c], cmul(a[i * 64 + kk], x[kk * 64 + c]));
+      const double2 l = a[i * 64 + kk];
+      x[i * 64 + c] = csub(x[i * 64 + c], cmul(make_double2(l.x * inv, l.y * inv), x[kk * 64 + c]));
     }
     __syncthreads();
   }
   double2* dst = Linv + (long long)k * M * M;
-  for (int e = tid; e < M * M; e += 256) dst[e] = x[(e / M) * 64 + (e % M)];
+  for (int e = tid; e < M * M; e += 256) {
+    const int r = e / M, c = e % M;
+    const double2 v = x[r * 64 + c];
+    dst[e] = make_double2(v.x / piv[r], v.y / piv[r]);
+  }
   if (tid == 0) {
     double ld = 0.0;
-    for (int i = 0; i < M; ++i) ld += log(x[i * 64 + i].x);
+    for (int i = 0; i < M; ++i) ld += log(1.0 / piv[i]);
     cconst[k] = -(M * log(3.14159265358979323846)) + 2.0 * ld + logw[k];
     status[k] = 0;
   }
