@@ -152,6 +152,15 @@ int qce_model_set_option(qce_model* model, int option, double value);
 int qce_estimate_assigned(qce_model* model, const double* y, int64_t B, const int64_t* comp, double* h_out, int io,
                           void* stream);
 
+/* Toeplitz / block-Toeplitz inverse-EM covariance step (gmm_cplx_bussgang.py:792-826, Barton & Fuhrmann):
+ * S (K,N,N) c128 = the M-step's weighted sample covariances WITHOUT reg; F2 (P,N) c128 the partial DFT of
+ * `fit` (:143-153); sigma (K,P) f64 in/out.  init != 0 (_initialize, :582-586): sigma = max(Re diag(F2 S F2^H), reg),
+ * `model` unused.  init == 0: `model` is prepared on the previous covariances (A = NULL, snr = inf, n_bits = inf:
+ * its L^-1 gives Cinv); sigma += sigma^2 Re diag(F2 (Cinv S Cinv - Cinv) F2^H), max reg;
+ * covs_out (K,N,N) = F2^H diag(sigma) F2 + reg I.  Host buffers; synchronous. */
+int qce_em_toeplitz(qce_model* model, const double* S, int K, int N, const double* F2, int P, double* sigma, double reg,
+                    int init, double* covs_out, int device, void* stream);
+
 /* Device synchronisation of the model's stream (for timing and for QCE_IO_DEVICE callers). */
 int qce_synchronize(qce_model* model);
 

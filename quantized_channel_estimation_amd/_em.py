@@ -63,12 +63,13 @@ class DeviceEM:
     def _stream(self):
         return _torch().cuda.current_stream(self.dev).cuda_stream
 
-    def mstep(self, resp=None):
+    def mstep(self, resp=None, reg=None):
         """estimate_gaussian_parameters (:698-737) on the device; resp None = the last E-step's."""
         torch = _torch()
+        reg = self.reg if reg is None else float(reg)
         R = self.R if resp is None else torch.as_tensor(np.ascontiguousarray(resp, dtype=np.float64),
                                                         device=self.dev)
-        _lib.check(_lib.load().qce_em_mstep(_lib.ptr(self.X), self.B, self.N, self.K, _lib.ptr(R), self.reg,
+        _lib.check(_lib.load().qce_em_mstep(_lib.ptr(self.X), self.B, self.N, self.K, _lib.ptr(R), reg,
                                             int(self.diag), int(self.zero_mean), _lib.ptr(self.nk),
                                             _lib.ptr(self.mu), _lib.ptr(self.cov), self.device, _lib.IO_DEVICE,
                                             self._stream()))
@@ -94,6 +95,20 @@ class DeviceEM:
             _torch().cuda.current_stream(self.dev).synchronize()
             self._dm.close()
             self._dm = None
+
+    def toeplitz_step(self, S, F2, sigma, init):
+        """Inverse-EM covariance step (:792-826); init: the Sigma of _initialize (:582-586).
+        Returns (sigma, covariances or None)."""
+        S = np.ascontiguousarray(S, dtype=np.complex128)
+        F2 = np.ascontiguousarray(F2, dtype=np.complex128)
+        sigma = np.ascontiguousarray(sigma, dtype=np.float64).copy()
+        covs = None if init else np.empty((self.K, self.N, self.N), dtype=np.complex128)
+        _torch().cuda.current_stream(self.dev).synchronize()
+        h = None if init else self._dm.handle
+        _lib.check(_lib.load().qce_em_toeplitz(h, _lib.ptr(S), self.K, self.N, _lib.ptr(F2), F2.shape[0],
+                                               _lib.ptr(sigma), self.reg, int(init), _lib.ptr(covs), self.device,
+                                               None if init else self._stream()))
+        return sigma, covs
 
     def labels(self):
         return self.R.argmax(dim=1).cpu().numpy()
@@ -128,8 +143,7 @@ def fit_predict(obj, X):
         raise ValueError("Unimplemented initialization method '%s'" % gm.init_params)
     if getattr(gm, "precisions_init", None) is not None:
         raise NotImplementedError("precisions_init is not supported by the device EM")
-    if "inv-em" in obj.params:
-        raise NotImplementedError("Toeplitz-structured (inv-em) fitting is not provided by the device EM")
+    inv_em = "inv-em" in obj.params
     K = gm.n_components
     do_init = not (gm.warm_start and hasattr(obj, "converged_"))  # the reference tests the wrapper (:491)
     n_init = gm.n_init if do_init else 1
@@ -147,7 +161,11 @@ def fit_predict(obj, X):
         for n_iter in range(1, gm.max_iter + 1):
             prev_lower_bound = lower_bound
             log_prob_norm = em.estep(gm.means_, full_of(gm.covariances_, em.diag), gm.weights_)
-            nk, means, cov = em.mstep()
+            if inv_em:  # estimate_gaussian_covariances_inv (:792-826)
+                nk, means, S = em.mstep(reg=0.0)
+                gm.Sigma, cov = em.toeplitz_step(S, obj.F2, gm.Sigma, init=False)
+            else:
+                nk, means, cov = em.mstep()
             gm.weights_, gm.means_, gm.covariances_ = nk / n_samples, means, cov
             lower_bound = log_prob_norm
             change = lower_bound - prev_lower_bound
@@ -197,3 +215,5 @@ def _initialize_parameters(obj, em, X, random_state):
     gm.weights_ = weights if gm.weights_init is None else gm.weights_init
     gm.means_ = means if gm.means_init is None else gm.means_init
     gm.covariances_ = cov
+    if "inv-em" in obj.params:  # :582-586
+        gm.Sigma, _ = em.toeplitz_step(cov, obj.F2, np.zeros((gm.n_components, obj.F2.shape[0])), init=True)

@@ -1240,6 +1240,60 @@ int qce_estimate_assigned(qce_model* m, const double* y, int64_t B, const int64_
   return QCE_OK;
 }
 
+int qce_em_toeplitz(qce_model* m, const double* S, int K, int N, const double* F2, int P, double* sigma, double reg,
+                    int init, double* covs_out, int device, void* stream) {
+  if (!S || !F2 || !sigma || K < 1 || N < 1 || P < 1 || (!init && (!m || !covs_out)))
+    return fail(QCE_EARG, "em_toeplitz: bad arguments");
+  int rc;
+  if (!init) {
+    if ((rc = check_model(m, true))) return rc;
+    if (m->K != K || m->N != N || m->M != N) return fail(QCE_EARG, "em_toeplitz: model shape mismatch");
+    if ((rc = ensure_dense(m))) return rc;
+    device = m->device;
+  }
+  DeviceGuard g(device);
+  hipStream_t st = (!init && !stream) ? m->stream : (hipStream_t)stream;
+  const size_t nn = (size_t)N * N, KNN = (size_t)K * nn;
+  const double2 one = make_double2(1.0, 0.0), zero = make_double2(0.0, 0.0), mone = make_double2(-1.0, 0.0);
+  {
+    StreamScratch sc(st);
+    void *dS, *dF, *dsg, *dG, *dC = nullptr, *dT = nullptr, *dM = nullptr;
+    HIPCHK(sc.get(&dS, sizeof(double2) * KNN));
+    HIPCHK(sc.get(&dF, sizeof(double2) * (size_t)P * N));
+    HIPCHK(sc.get(&dsg, sizeof(double) * (size_t)K * P));
+    HIPCHK(sc.get(&dG, sizeof(double2) * (size_t)K * P * N));
+    HIPCHK(hipMemcpyAsync(dS, S, sizeof(double2) * KNN, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dF, F2, sizeof(double2) * (size_t)P * N, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dsg, sigma, sizeof(double) * (size_t)K * P, hipMemcpyHostToDevice, st));
+    const double2* Mx = (const double2*)dS;
+    if (!init) {
+      // Cinv = Linv^H Linv (the previous covariances' inverse, :808); Mx = Cinv S Cinv - Cinv (:812)
+      HIPCHK(sc.get(&dC, sizeof(double2) * KNN));
+      HIPCHK(sc.get(&dT, sizeof(double2) * KNN));
+      HIPCHK(sc.get(&dM, sizeof(double2) * KNN));
+      HIPCHK(qce_zgemm_batched(2, 0, N, N, N, one, m->Linv.p, N, nn, m->Linv.p, N, nn, zero, (double2*)dC, N, nn, K,
+                               st));
+      HIPCHK(qce_zgemm_batched(0, 0, N, N, N, one, (const double2*)dC, N, nn, (const double2*)dS, N, nn, zero,
+                               (double2*)dT, N, nn, K, st));
+      HIPCHK(hipMemcpyAsync(dM, dC, sizeof(double2) * KNN, hipMemcpyDeviceToDevice, st));
+      HIPCHK(qce_zgemm_batched(0, 0, N, N, N, one, (const double2*)dT, N, nn, (const double2*)dC, N, nn, mone,
+                               (double2*)dM, N, nn, K, st));
+      Mx = (const double2*)dM;
+    }
+    // G_k = F2 Mx_k (P x N), then theta = Re diag(G_k F2^H)
+    HIPCHK(qce_zgemm_batched(0, 0, P, N, N, one, (const double2*)dF, N, 0, Mx, N, nn, zero, (double2*)dG, N,
+                             (long long)P * N, K, st));
+    HIPCHK(qce_launch_inv_em_sigma(K, N, P, (const double2*)dG, (const double2*)dF, (double*)dsg, reg, init, st));
+    HIPCHK(hipMemcpyAsync(sigma, dsg, sizeof(double) * (size_t)K * P, hipMemcpyDeviceToHost, st));
+    if (!init) {
+      HIPCHK(qce_launch_inv_em_cov(K, N, P, (const double2*)dF, (const double*)dsg, reg, (double2*)dT, st));
+      HIPCHK(hipMemcpyAsync(covs_out, dT, sizeof(double2) * KNN, hipMemcpyDeviceToHost, st));
+    }
+  }
+  HIPCHK(hipStreamSynchronize(st));
+  return QCE_OK;
+}
+
 int qce_synchronize(qce_model* m) {
   if (!m) return fail(QCE_EARG, "null model");
   DeviceGuard g(m->device);

@@ -225,6 +225,60 @@ __global__ __launch_bounds__(64) void k_mean_final(long long n, const double* __
 
 }  // namespace
 
+namespace {
+
+// one thread per (component, frequency p): theta = Re sum_j G[k][p][j] conj(F2[p][j])   (G = F2 Mx_k)
+__global__ __launch_bounds__(256) void k_inv_em_sigma(int K, int N, int P, const double2* __restrict__ G,
+                                                      const double2* __restrict__ F2, double* __restrict__ sigma,
+                                                      double reg, int init) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long long)K * P) return;
+  const int k = (int)(e / P), p = (int)(e % P);
+  const double2* g = G + ((long long)k * P + p) * N;
+  const double2* f = F2 + (long long)p * N;
+  double th = 0.0;
+  for (int j = 0; j < N; ++j) th += g[j].x * f[j].x + g[j].y * f[j].y;
+  double sg = init ? th : sigma[e] + sigma[e] * th * sigma[e];  // Sigma + Sigma * Theta * Sigma (:821)
+  if (sg < reg) sg = reg;                                           // (:822, and :585 at init)
+  sigma[e] = sg;
+}
+
+// C_k[i][j] = sum_p conj(F2[p][i]) sigma_kp F2[p][j] + reg [i == j]   (:823-824)
+__global__ __launch_bounds__(256) void k_inv_em_cov(int K, int N, int P, const double2* __restrict__ F2,
+                                                    const double* __restrict__ sigma, double reg,
+                                                    double2* __restrict__ C) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (long long)K * N * N) return;
+  const int k = (int)(e / ((long long)N * N));
+  const int rc = (int)(e - (long long)k * N * N), i = rc / N, j = rc % N;
+  const double* sg = sigma + (long long)k * P;
+  double2 acc = make_double2(0.0, 0.0);
+  for (int p = 0; p < P; ++p) {
+    const double2 a = F2[(long long)p * N + i], b = F2[(long long)p * N + j];
+    const double2 ca = make_double2(a.x * sg[p], -a.y * sg[p]);
+    acc = cfma(ca, b, acc);
+  }
+  if (i == j) acc.x += reg;
+  C[e] = acc;
+}
+
+}  // namespace
+
+hipError_t qce_launch_inv_em_sigma(int K, int N, int P, const double2* G, const double2* F2, double* sigma, double reg,
+                                   int init, hipStream_t st) {
+  const long long n = (long long)K * P;
+  hipLaunchKernelGGL(k_inv_em_sigma, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, N, P, G, F2, sigma, reg,
+                     init);
+  return hipGetLastError();
+}
+
+hipError_t qce_launch_inv_em_cov(int K, int N, int P, const double2* F2, const double* sigma, double reg, double2* C,
+                                 hipStream_t st) {
+  const long long n = (long long)K * N * N;
+  hipLaunchKernelGGL(k_inv_em_cov, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, K, N, P, F2, sigma, reg, C);
+  return hipGetLastError();
+}
+
 QceEmPlan qce_em_plan(long long B, int N, int K, int diag) {
   QceEmPlan p;
   p.C = (int)((B + STAT_CHUNK - 1) / STAT_CHUNK);

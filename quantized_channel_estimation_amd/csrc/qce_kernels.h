@@ -207,3 +207,16 @@ hipError_t qce_launch_em_resp(long long B, int K, const double* lp, double* resp
 // h_b = W_c y_b + b_c with c = comp[b] (comp == nullptr: c = b) — per-sample ("genie") filters
 hipError_t qce_launch_est_assigned(long long B, int N, int M, int K, const double2* y, const long long* comp,
                                    const double2* W, const double2* bvec, double2* h, hipStream_t st);
+
+// batched row-major complex GEMM C = alpha op(A) op(B) + beta C (op 0 = N, 1 = T, 2 = C^H); supported
+// (opa, opb): (0,0) (0,2) (2,0) (0,1).  Strides sA/sB/sC per batch entry (0 = shared operand).
+hipError_t qce_zgemm_batched(int opa, int opb, int m, int n, int k, double2 alpha, const double2* A, int lda,
+                             long long sA, const double2* B, int ldb, long long sB, double2 beta, double2* C, int ldc,
+                             long long sC, int batch, hipStream_t st);
+// Toeplitz inverse-EM covariance step (qce_em.hip; gmm_cplx_bussgang.py:792-826)
+//   theta_kp = Re diag(F2 Mx_k F2^H)_p; init: sigma = max(theta, reg); else sigma += sigma^2 theta, max reg
+hipError_t qce_launch_inv_em_sigma(int K, int N, int P, const double2* G, const double2* F2, double* sigma, double reg,
+                                   int init, hipStream_t st);
+//   C_k = F2^H diag(sigma_k) F2 + reg I
+hipError_t qce_launch_inv_em_cov(int K, int N, int P, const double2* F2, const double* sigma, double reg, double2* C,
+                                 hipStream_t st);

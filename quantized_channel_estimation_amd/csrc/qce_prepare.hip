@@ -104,6 +104,12 @@ static hipError_t zgemm(int opa, int opb, int m, int n, int k, double2 alpha, co
   return hipErrorInvalidValue;
 }
 
+hipError_t qce_zgemm_batched(int opa, int opb, int m, int n, int k, double2 alpha, const double2* A, int lda,
+                             long long sA, const double2* B, int ldb, long long sB, double2 beta, double2* C, int ldc,
+                             long long sC, int batch, hipStream_t st) {
+  return zgemm(opa, opb, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batch, st);
+}
+
 // Cy = C + s2 I  (A = I fast path; numerically identical to I C I^H + s2 I)
 __global__ void k_cy_identity(int N, long long total, const double2* __restrict__ C, double2* __restrict__ Cy, double s2) {
   long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;

@@ -113,8 +113,8 @@ class Gmm_nbit:
         """EM training on the device (gmm_cplx_bussgang.py:96-163).
 
         'full': EM on h.  'circulant' / 'block-circulant': EM with diagonal covariances on the
-        (block-)DFT of h, then C_k = F^H diag(c_k) F (:104-134).  The Toeplitz variants use the
-        reference's inverse-EM M-step (:792-826), which is not provided: NotImplementedError."""
+        (block-)DFT of h, then C_k = F^H diag(c_k) F (:104-134).  'toeplitz' / 'block-toeplitz': the
+        inverse-EM M-step (:792-826) with the partial DFT F2 (:143-163)."""
         from . import _em
         self.params["zero_mean"] = bool(zero_mean)
         h = np.asarray(h)
@@ -143,8 +143,26 @@ class Gmm_nbit:
             self.means_cplx = self.gm.means_.copy()
             self.covs_cplx = self.gm.covariances_.copy()
             self.chol = self.gm.precisions_cholesky_.copy()
-        elif ct in ("toeplitz", "block-toeplitz"):
-            raise NotImplementedError(f"Fitting for covariance_type = {ct} (inverse EM) is not provided on the device")
+        elif ct == "toeplitz":  # :143-151
+            self.params["inv-em"] = True
+            self.gm.covariance_type = "full"
+            n_1 = h.shape[1]
+            self.F2 = np.fft.fft(np.eye(2 * n_1))[:, :n_1] / np.sqrt(2 * n_1)
+            self.fit_cplx(h)
+            self.means_cplx = self.gm.means_.copy()
+            self.covs_cplx = self.gm.covariances_.copy()
+            self.chol = self.gm.precisions_cholesky_.copy()
+        elif ct == "block-toeplitz":  # :152-163
+            self.params["inv-em"] = True
+            self.gm.covariance_type = "full"
+            n_1, n_2 = blocks
+            F2_1 = np.fft.fft(np.eye(2 * n_1))[:, :n_1] / np.sqrt(2 * n_1)
+            F2_2 = np.fft.fft(np.eye(2 * n_2))[:, :n_2] / np.sqrt(2 * n_2)
+            self.F2 = np.kron(F2_1, F2_2)
+            self.fit_cplx(h)
+            self.means_cplx = self.gm.means_.copy()
+            self.covs_cplx = self.gm.covariances_.copy()
+            self.chol = self.gm.precisions_cholesky_.copy()
         else:
             raise NotImplementedError(f"Fitting for covariance_type = {ct} is not implemented.")
         return self

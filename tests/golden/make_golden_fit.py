@@ -36,11 +36,18 @@ def main():
         ("circ", "circulant", None, True, dict(n_components=6, random_state=0, max_iter=12)),
         ("bcirc", "block-circulant", (2, 8), False, dict(n_components=5, random_state=3, max_iter=12)),
         ("full_ninit", "full", None, True, dict(n_components=4, random_state=5, max_iter=6, n_init=2)),
+        ("toep", "toeplitz", None, True, dict(n_components=5, random_state=0, max_iter=10)),
+        ("btoep", "block-toeplitz", (2, 8), False, dict(n_components=4, random_state=4, max_iter=8)),
     ]
     tags = []
+    from threadpoolctl import threadpool_limits
     for tag, ct, blocks, zm, kw in cases:
         g = gmm_mod.Gmm_nbit(covariance_type=ct, **kw)
-        g.fit(h16, blocks=blocks, zero_mean=zm)
+        # sklearn's threaded K-means adds per-thread partial centres in completion order, so its
+        # labels (and the whole EM trajectory after them) can change from run to run: one thread here
+        # and in the test keeps the initialisation reproducible.
+        with threadpool_limits(limits=1):
+            g.fit(h16, blocks=blocks, zero_mean=zm)
         p = tag + "__"
         out[p + "cov_type"] = np.array(ct)
         out[p + "blocks"] = np.array(blocks if blocks else (0, 0))
@@ -54,6 +61,8 @@ def main():
         out[p + "lower_bound"] = np.float64(g.gm.lower_bound_)
         out[p + "converged"] = np.bool_(g.gm.converged_)
         out[p + "chol"] = np.asarray(g.chol)
+        if getattr(g.gm, "Sigma", None) is not None:
+            out[p + "Sigma"] = np.asarray(g.gm.Sigma)
         if g.fft_covs is not None:
             out[p + "fft_covs"] = np.asarray(g.fft_covs)
             out[p + "fft_means"] = np.asarray(g.fft_means)

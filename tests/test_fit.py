@@ -31,9 +31,9 @@ def test_oracle_mstep_matches_reference(fx):
     assert not mu0.any() and rel_fro(cov0, fx["mstep_covs_zm"]) < 1e-13
 
 
-def test_fit_rejects_toeplitz_on_cpu_without_device_work():
+def test_fit_rejects_unknown_covariance_type_without_device_work():
     from quantized_channel_estimation_amd import Gmm_nbit
-    g = Gmm_nbit(n_components=2, covariance_type="toeplitz")
+    g = Gmm_nbit(n_components=2, covariance_type="tied")
     with pytest.raises(NotImplementedError):
         g.fit(np.zeros((10, 4), complex))
 
@@ -103,24 +103,33 @@ def _kw(fx, tag):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("tag", ["full_zm", "full_mean", "full_rand", "circ", "bcirc", "full_ninit"])
+@pytest.mark.parametrize("tag", ["full_zm", "full_mean", "full_rand", "circ", "bcirc", "full_ninit", "toep", "btoep"])
 def test_gpu_fit_matches_reference(fx, tag):
     import warnings
     from quantized_channel_estimation_amd import Gmm_nbit
     p = tag + "__"
     ct = str(fx[p + "cov_type"])
     blocks = tuple(int(v) for v in fx[p + "blocks"])
+    from threadpoolctl import threadpool_limits
     g = Gmm_nbit(covariance_type=ct, **_kw(fx, tag))
-    with warnings.catch_warnings():
+    with warnings.catch_warnings(), threadpool_limits(limits=1):  # deterministic K-means (make_golden_fit.py)
         warnings.simplefilter("ignore")
         g.fit(fx["h16"], blocks=blocks if blocks[0] else None, zero_mean=bool(fx[p + "zero_mean"]))
-    assert g.gm.n_iter_ == int(fx[p + "n_iter"])
-    assert bool(g.gm.converged_) == bool(fx[p + "converged"])
-    assert abs(g.gm.lower_bound_ - float(fx[p + "lower_bound"])) <= 1e-8 * max(1.0, abs(float(fx[p + "lower_bound"])))
-    assert rel_fro(g.gm.weights_, fx[p + "weights"]) < 1e-7
-    assert rel_fro(g.means_cplx, fx[p + "means_cplx"]) < 1e-6 or np.abs(fx[p + "means_cplx"]).max() < 1e-12
-    assert rel_fro(g.covs_cplx, fx[p + "covs_cplx"]) < 1e-7
-    assert rel_fro(g.chol, fx[p + "chol"]) < 1e-5
+    info = (g.gm.n_iter_, g.gm.lower_bound_, float(fx[p + "lower_bound"]))
+    # The inverse EM (toeplitz, :792-826) subtracts nearly equal terms (Cinv S Cinv - Cinv, cond(C) ~ 6e6
+    # here): the reference's own arithmetic moves its lower bound by 2.6e-5 when np.linalg.pinv is
+    # replaced by np.linalg.inv (measured, same data), so its bar is set at that scale.
+    inv_em = "toep" in tag
+    t_lb, t_par, t_chol = (2e-5, 1e-3, 1e-2) if inv_em else (1e-8, 1e-7, 1e-5)
+    assert g.gm.n_iter_ == int(fx[p + "n_iter"]), info
+    assert bool(g.gm.converged_) == bool(fx[p + "converged"]), info
+    assert abs(g.gm.lower_bound_ - float(fx[p + "lower_bound"])) <= t_lb * max(1.0, abs(float(fx[p + "lower_bound"]))), info
+    assert rel_fro(g.gm.weights_, fx[p + "weights"]) < t_par
+    assert rel_fro(g.means_cplx, fx[p + "means_cplx"]) < 10 * t_par or np.abs(fx[p + "means_cplx"]).max() < 1e-12
+    assert rel_fro(g.covs_cplx, fx[p + "covs_cplx"]) < t_par
+    assert rel_fro(g.chol, fx[p + "chol"]) < t_chol
+    if (p + "Sigma") in fx:
+        assert rel_fro(g.gm.Sigma, fx[p + "Sigma"]) < t_par
     if (p + "fft_covs") in fx:
         assert rel_fro(g.fft_covs, fx[p + "fft_covs"].real) < 1e-7
     assert g.gm.covariance_type == "full"
