@@ -161,6 +161,15 @@ int qce_estimate_assigned(qce_model* model, const double* y, int64_t B, const in
 int qce_em_toeplitz(qce_model* model, const double* S, int K, int N, const double* F2, int P, double* sigma, double reg,
                     int init, double* covs_out, int device, void* stream);
 
+/* SCM multi-path channels (modules/SCM3GPP/SCMMulti.py:30-56 generate_channel, scm_helper.py:17-84):
+ * h_out (B, n_coherence, N) complex64, t_out (B, N) complex64 (first covariance rows).  gains / angles
+ * (B, n_path) f64 (normalised gains, angles in degrees) and x (B, 100 N, n_coherence) c128 (the crandn draw)
+ * may be supplied — the reference's own draws give its channels to float32 rounding — or NULL: then drawn on the
+ * device from Philox4x32-10 keyed by `seed`.  N <= 256, n_path <= 16.  Buffers where `io` says. */
+int qce_scm_generate(int64_t B, int n_coherence, int N, int n_path, double path_sigma, const double* gains,
+                     const double* angles, const double* x, uint64_t seed, float* h_out, float* t_out, int device,
+                     int io, void* stream);
+
 /* Device synchronisation of the model's stream (for timing and for QCE_IO_DEVICE callers). */
 int qce_synchronize(qce_model* model);
 

@@ -33,6 +33,8 @@ SIGNATURES = {
     "qce_model_set_params": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
     "qce_em_toeplitz": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int, _vp, ctypes.c_double,
                                        ctypes.c_int, _vp, ctypes.c_int, _vp]),
+    "qce_scm_generate": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, _vp,
+                                        _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, ctypes.c_int, _vp]),
     "qce_model_set_option": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double]),
     "qce_estimate_assigned": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp]),
     "qce_prepare": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int, _vp, _vp,

@@ -1294,6 +1294,52 @@ int qce_em_toeplitz(qce_model* m, const double* S, int K, int N, const double* F
   return QCE_OK;
 }
 
+int qce_scm_generate(int64_t B, int n_coherence, int N, int n_path, double path_sigma, const double* gains,
+                     const double* angles, const double* x, uint64_t seed, float* h_out, float* t_out, int device,
+                     int io, void* stream) {
+  if (B < 0 || n_coherence < 1 || N < 1 || N > 256 || n_path < 1 || n_path > qce_scm_max_path() ||
+      (B > 0 && (!h_out || !t_out)) || (!gains) != (!angles))
+    return fail(QCE_EARG, "scm_generate: bad arguments");
+  if (io != QCE_IO_HOST && io != QCE_IO_DEVICE) return fail(QCE_EARG, "scm_generate: bad io");
+  if (B == 0) return QCE_OK;
+  DeviceGuard g(device);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t F = 100 * (size_t)N, nh = (size_t)B * n_coherence * N, nt = (size_t)B * N;
+  {
+    StreamScratch sc(st);
+    void* p;
+    const double *dg = gains, *da = angles;
+    const double2* dx = (const double2*)x;
+    float2* dh = (float2*)h_out;
+    float2* dt = (float2*)t_out;
+    if (io == QCE_IO_HOST) {
+      if (gains) {
+        HIPCHK(sc.get(&p, sizeof(double) * 2 * (size_t)B * n_path));
+        HIPCHK(hipMemcpyAsync(p, gains, sizeof(double) * (size_t)B * n_path, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync((double*)p + (size_t)B * n_path, angles, sizeof(double) * (size_t)B * n_path,
+                              hipMemcpyHostToDevice, st));
+        dg = (const double*)p;
+        da = (const double*)p + (size_t)B * n_path;
+      }
+      if (x) {
+        HIPCHK(sc.get(&p, sizeof(double2) * (size_t)B * F * n_coherence));
+        HIPCHK(hipMemcpyAsync(p, x, sizeof(double2) * (size_t)B * F * n_coherence, hipMemcpyHostToDevice, st));
+        dx = (const double2*)p;
+      }
+      HIPCHK(sc.get(&p, sizeof(float2) * (nh + nt)));
+      dh = (float2*)p;
+      dt = (float2*)p + nh;
+    }
+    HIPCHK(qce_launch_scm(B, n_coherence, N, n_path, path_sigma, dg, da, dx, seed, dh, dt, st));
+    if (io == QCE_IO_HOST) {
+      HIPCHK(hipMemcpyAsync(h_out, dh, sizeof(float2) * nh, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(t_out, dt, sizeof(float2) * nt, hipMemcpyDeviceToHost, st));
+    }
+  }
+  if (io == QCE_IO_HOST) HIPCHK(hipStreamSynchronize(st));
+  return QCE_OK;
+}
+
 int qce_synchronize(qce_model* m) {
   if (!m) return fail(QCE_EARG, "null model");
   DeviceGuard g(m->device);

@@ -220,3 +220,9 @@ hipError_t qce_launch_inv_em_sigma(int K, int N, int P, const double2* G, const 
 //   C_k = F2^H diag(sigma_k) F2 + reg I
 hipError_t qce_launch_inv_em_cov(int K, int N, int P, const double2* F2, const double* sigma, double reg, double2* C,
                                  hipStream_t st);
+
+// SCM channels (qce_scm.hip; scm_helper.py:17-84, SCMMulti.py:30-56)
+int qce_scm_max_path();
+hipError_t qce_launch_scm(long long B, int n_coh, int N, int n_path, double sigma, const double* gains,
+                          const double* angles, const double2* x, unsigned long long seed, float2* h, float2* t,
+                          hipStream_t st);
