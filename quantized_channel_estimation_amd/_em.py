@@ -88,6 +88,9 @@ class DeviceEM:
         self._dm.prepare(None, float("inf"), float("inf"), stream=self._stream())
         _lib.check(_lib.load().qce_em_estep(self._dm.handle, _lib.ptr(self.X), self.B, _lib.ptr(self.R),
                                             _lib.ptr(self.lse), _lib.IO_DEVICE, self._stream()))
+        # torch's default stream has handle 0, which the model-bound entry points read as "the model's own
+        # (non-blocking) stream": finish that stream before torch-side reads of R / lse
+        self._dm.synchronize()
         return float(self.lse.cpu().numpy()[0])
 
     def close(self):

@@ -62,6 +62,9 @@ int pad_dim(int v) {
 
 struct qce_model {
   int K = 0, N = 0, device = 0;
+  int a_identity_n = 0;   // m->A holds I_N (skips the upload + sync of a repeated A = NULL prepare)
+  int packs_valid = 0;    // pack32 / pack64 built for the current prepare (lazy: 'all' mode never needs them)
+  QcePrepareArgs pack_args{};
   int beta_first = 0;  // QCE_OPT_BETA_FIRST: multi-bit Cr mixes with the first gain (blmmse.py:53, :86)
   hipStream_t stream = nullptr;
   int has_mean = 0;
@@ -149,6 +152,13 @@ int stage_input(qce_model* m, const double* y, long long B, int io, hipStream_t 
   HIPCHK(m->y_scr.ensure((size_t)B * m->M));
   HIPCHK(hipMemcpyAsync(m->y_scr.p, y, sizeof(double2) * (size_t)B * m->M, hipMemcpyHostToDevice, st));
   *dy = m->y_scr.p;
+  return QCE_OK;
+}
+
+int ensure_packs(qce_model* m, hipStream_t st) {
+  if (m->packs_valid) return QCE_OK;
+  HIPCHK(qce_launch_pack_selective(m->pack_args, st));
+  m->packs_valid = 1;
   return QCE_OK;
 }
 
@@ -657,11 +667,15 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
   int identityA = 0;
   if (A) {
     HIPCHK(hipMemcpyAsync(m->A.p, A, sizeof(double2) * (size_t)M * N, hipMemcpyHostToDevice, st));
+    m->a_identity_n = 0;
   } else {
-    std::vector<double> eye((size_t)2 * N * N, 0.0);
-    for (int i = 0; i < N; ++i) eye[(size_t)2 * (i * N + i)] = 1.0;
-    HIPCHK(hipMemcpyAsync(m->A.p, eye.data(), sizeof(double2) * (size_t)N * N, hipMemcpyHostToDevice, st));
-    HIPCHK(hipStreamSynchronize(st));
+    if (m->a_identity_n != N) {
+      std::vector<double> eye((size_t)2 * N * N, 0.0);
+      for (int i = 0; i < N; ++i) eye[(size_t)2 * (i * N + i)] = 1.0;
+      HIPCHK(hipMemcpyAsync(m->A.p, eye.data(), sizeof(double2) * (size_t)N * N, hipMemcpyHostToDevice, st));
+      HIPCHK(hipStreamSynchronize(st));
+      m->a_identity_n = N;
+    }
     identityA = 1;
   }
   if (A && M == N) {  // an explicit identity takes the same fast path (bitwise the same Cy)
@@ -723,6 +737,10 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
   p.stride32 = s32;
   p.pack64 = m->pack64.p;
   p.stride64 = s64;
+  m->pack_args = p;
+  m->packs_valid = 0;
+  p.pack32 = nullptr;  // selective-mode / log-prob tables are packed on first use (ensure_packs)
+  p.pack64 = nullptr;
   HIPCHK(qce_launch_prepare(p, st));
   // FP16 two-term split tables; the observation scale makes quantiser outputs exact in fp16
   // (1 bit: y sqrt(2) = +-1; uniform: y 2/delta = odd integers), folded into the slice scales
@@ -775,6 +793,7 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
     HIPCHK(m->h_scr.ensure((size_t)B * m->N));
     dh = m->h_scr.p;
   }
+  if (!m->fft_active && (mode != QCE_MODE_ALL || !use_h2()) && (rc = ensure_packs(m, st))) return rc;
   QceEstArgs a = est_args(m, dy, B);
   if (m->fft_active) {  // Fourier-domain path (qce_fft.hip)
     QceFftEstArgs fa = fft_args(m, dy, B);
@@ -846,6 +865,7 @@ int qce_log_prob(qce_model* m, const double* X, int64_t B, double* lp_out, doubl
   hipStream_t st = pick_stream(m, stream);
   const double2* dx = nullptr;
   if ((rc = stage_input(m, X, B, io, st, &dx))) return rc;
+  if (!m->fft_active && (rc = ensure_packs(m, st))) return rc;
   QceEstArgs a = est_args(m, dx, B);
   const size_t BK = (size_t)B * m->K;
   double* dlp = lp_out;
@@ -910,6 +930,7 @@ int qce_estimate_partial(qce_model* m, const double* y, int64_t B, double* m_out
   } else if (use_h2() || !qce_shape_supported(m->MP, m->NP)) {
     if ((rc = run_h2(m, dy, B, nullptr, dm, ds, da, st))) return rc;
   } else {
+    if ((rc = ensure_packs(m, st))) return rc;
     QceEstArgs a = est_args(m, dy, B);
     HIPCHK(qce_launch_est_partial(a, dm, ds, da, st));
   }
@@ -1111,6 +1132,7 @@ int qce_em_estep(qce_model* m, const double* X, int64_t B, double* resp_out, dou
     fa.lp = dlp;
     HIPCHK(qce_launch_fft_est(fa, 1, st));
   } else {
+    if ((rc = ensure_packs(m, st))) return rc;
     QceEstArgs a = est_args(m, dx, B);
     HIPCHK(qce_launch_lp(a, dlp, st));
   }

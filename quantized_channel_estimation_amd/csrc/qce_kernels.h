@@ -27,6 +27,7 @@ struct QcePrepareArgs {
 long long qce_pack_f32_stride(int MP, int NP, int has_mean);
 long long qce_pack_f64_stride(int MP, int has_mean);
 hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st);
+hipError_t qce_launch_pack_selective(const QcePrepareArgs& p, hipStream_t st);
 
 struct QceEstArgs {
   long long B;

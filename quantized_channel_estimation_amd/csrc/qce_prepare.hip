@@ -528,6 +528,14 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
     return e;
   if ((e = zgemm(0, 0, N, 1, M, mone, p.V, M, (long long)N * M, p.q0, 1, M, one, p.bvec, 1, N, K, st)) != hipSuccess)
     return e;
+  return qce_launch_pack_selective(p, st);
+}
+
+// FP32 / FP64 fragment-order tables of the selective modes and the log-prob kernel (skipped when the
+// pointers are null; the C-ABI layer runs this lazily on the first call that needs them)
+hipError_t qce_launch_pack_selective(const QcePrepareArgs& p, hipStream_t st) {
+  const int K = p.K, N = p.N, M = p.M;
+  hipError_t e;
   // pack
   if (p.pack32) {
     const int nsl = (2 * p.MP) / 32 + (2 * p.NP) / 32;
