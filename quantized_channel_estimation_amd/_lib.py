@@ -191,8 +191,23 @@ class DeviceModel:
             out = torch.empty((B, self.N), dtype=torch.complex128, device=y.device)
         if y.shape[1] != self.M:
             raise ValueError(f"y must have {self.M} columns, got {y.shape[1]}")
+        self._order_before(y, io, stream)
         check(load().qce_estimate(self._h, ptr(y), int(B), int(mode), float(param), ptr(out), io, stream))
+        self._order_after(io, stream)
         return out
+
+    @staticmethod
+    def _order_before(y, io, stream):
+        """... and the inputs torch produced on its current stream must be complete before that stream runs."""
+        if io == IO_DEVICE and not stream:
+            import torch
+            torch.cuda.current_stream(y.device).synchronize()
+
+    def _order_after(self, io, stream):
+        """Device I/O without an explicit stream ran on the model's own non-blocking stream (a NULL
+        handle there means "the model's stream"): finish it so torch's streams see the results."""
+        if io == IO_DEVICE and not stream:
+            self.synchronize()
 
     def log_prob(self, X, want_lp=True, want_proba=False, want_labels=False):
         X = np.ascontiguousarray(X, dtype=np.complex128)
@@ -219,7 +234,9 @@ class DeviceModel:
             m_out = torch.empty(B, dtype=torch.float64, device=dev) if m_out is None else m_out
             s_out = torch.empty(B, dtype=torch.float64, device=dev) if s_out is None else s_out
             acc_out = torch.empty((B, 2 * self.N), dtype=torch.float32, device=dev) if acc_out is None else acc_out
+        self._order_before(y, io, stream)
         check(load().qce_estimate_partial(self._h, ptr(y), int(B), ptr(m_out), ptr(s_out), ptr(acc_out), io, stream))
+        self._order_after(io, stream)
         return m_out, s_out, acc_out
 
     def set_option(self, option, value):
