@@ -170,6 +170,15 @@ int qce_scm_generate(int64_t B, int n_coherence, int N, int n_path, double path_
                      const double* angles, const double* x, uint64_t seed, float* h_out, float* t_out, int device,
                      int io, void* stream);
 
+/* Statistical achievable-rate lower bound of the scripts (Bussgang_GMM.py:146-162 and its copies
+ * :206-216, :238-249, :291-306): g_b = h_est_b / max(||h_est_b||^2, norm_clip) (norm_clip 0: no clip; the
+ * GMM branch uses 0.1), inner_b = g_b^H diag(buss) h_b, den2_b = Re g_b^H Cq g_b;
+ * out[0] = log2(1 + num / (den1 + den2)), out[1] = num = |mean inner|^2, out[2] = den1 = var(inner),
+ * out[3] = den2 = mean den2_b.  h_est / h (B,N) c128 where `io` says; buss (N,) f64, Cq (N,N) c128 and out
+ * host; synchronous. */
+int qce_rate_bound(const double* h_est, const double* h, int64_t B, int N, const double* buss, const double* Cq,
+                   double norm_clip, double* out, int device, int io, void* stream);
+
 /* Device synchronisation of the model's stream (for timing and for QCE_IO_DEVICE callers). */
 int qce_synchronize(qce_model* model);
 

@@ -1362,6 +1362,43 @@ int qce_scm_generate(int64_t B, int n_coherence, int N, int n_path, double path_
   return QCE_OK;
 }
 
+int qce_rate_bound(const double* h_est, const double* h, int64_t B, int N, const double* buss, const double* Cq,
+                   double norm_clip, double* out, int device, int io, void* stream) {
+  if (B < 1 || N < 1 || !h_est || !h || !buss || !Cq || !out) return fail(QCE_EARG, "rate_bound: bad arguments");
+  if (io != QCE_IO_HOST && io != QCE_IO_DEVICE) return fail(QCE_EARG, "rate_bound: bad io");
+  DeviceGuard g(device);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t nb = (size_t)B * N;
+  {
+    StreamScratch sc(st);
+    void *dhe = (void*)h_est, *dh = (void*)h, *dbuss, *dcq, *inner, *den2, *part, *stat;
+    HIPCHK(sc.get(&dbuss, sizeof(double) * N));
+    HIPCHK(sc.get(&dcq, sizeof(double2) * (size_t)N * N));
+    HIPCHK(hipMemcpyAsync(dbuss, buss, sizeof(double) * N, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dcq, Cq, sizeof(double2) * (size_t)N * N, hipMemcpyHostToDevice, st));
+    HIPCHK(sc.get(&inner, sizeof(double2) * (size_t)B));
+    HIPCHK(sc.get(&den2, sizeof(double) * (size_t)B));
+    HIPCHK(sc.get(&part, sizeof(double) * qce_rate_scratch()));
+    HIPCHK(sc.get(&stat, sizeof(double) * 8));
+    if (io == QCE_IO_HOST) {
+      HIPCHK(sc.get(&dhe, sizeof(double2) * nb));
+      HIPCHK(sc.get(&dh, sizeof(double2) * nb));
+      HIPCHK(hipMemcpyAsync(dhe, h_est, sizeof(double2) * nb, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(dh, h, sizeof(double2) * nb, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(qce_launch_rate(B, N, (const double2*)dhe, (const double2*)dh, (const double*)dbuss, (const double2*)dcq,
+                           norm_clip, (double2*)inner, (double*)den2, (double*)part, (double*)stat, st));
+    double res[6];
+    HIPCHK(hipMemcpyAsync(res, stat, sizeof(double) * 6, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    out[0] = res[5];  // rate
+    out[1] = res[4];  // num
+    out[2] = res[3];  // den1
+    out[3] = res[2];  // den2
+  }
+  return QCE_OK;
+}
+
 int qce_synchronize(qce_model* m) {
   if (!m) return fail(QCE_EARG, "null model");
   DeviceGuard g(m->device);

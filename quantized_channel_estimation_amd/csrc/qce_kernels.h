@@ -227,3 +227,9 @@ int qce_scm_max_path();
 hipError_t qce_launch_scm(long long B, int n_coh, int N, int n_path, double sigma, const double* gains,
                           const double* angles, const double2* x, unsigned long long seed, float2* h, float2* t,
                           hipStream_t st);
+
+// statistical rate lower bound (qce_rate.hip; Bussgang_GMM.py:146-162)
+int qce_rate_scratch();
+hipError_t qce_launch_rate(long long B, int N, const double2* he, const double2* h, const double* buss,
+                           const double2* Cq, double clip, double2* inner, double* den2, double* part, double* stat,
+                           hipStream_t st);
