@@ -6,6 +6,6 @@ ctypes; there is no CPU fallback.
 """
 from .gmm import GaussianMixtureCplx, Gmm_nbit, Gmm_quant, mp_gmm  # noqa: F401
 from .mofa import Mofa  # noqa: F401
-from . import inputs, observe  # noqa: F401
+from . import baselines, experiment, inputs, observe, rate, scm  # noqa: F401
 
-__all__ = ["Gmm_nbit", "Gmm_quant", "GaussianMixtureCplx", "mp_gmm", "Mofa", "inputs", "observe"]
+__all__ = ["Gmm_nbit", "Gmm_quant", "GaussianMixtureCplx", "mp_gmm", "Mofa", "baselines", "experiment", "inputs", "observe", "rate", "scm"]
