@@ -152,6 +152,12 @@ int qce_model_set_option(qce_model* model, int option, double value);
 int qce_estimate_assigned(qce_model* model, const double* y, int64_t B, const int64_t* comp, double* h_out, int io,
                           void* stream);
 
+/* Bussgang least squares (estimators/LS.py: lstsq(A_eff, y)) with the prepared A_eff of component c = comp[b]
+ * (NULL: c = b).  Requires column-orthogonal A_eff (A = NULL or kron(x, I), the scripts' pilot matrices):
+ * h_i = sum_m conj(A_eff[m][i]) y_m / sum_m |A_eff[m][i]|^2. */
+int qce_estimate_ls(qce_model* model, const double* y, int64_t B, const int64_t* comp, double* h_out, int io,
+                    void* stream);
+
 /* Toeplitz / block-Toeplitz inverse-EM covariance step (gmm_cplx_bussgang.py:792-826, Barton & Fuhrmann):
  * S (K,N,N) c128 = the M-step's weighted sample covariances WITHOUT reg; F2 (P,N) c128 the partial DFT of
  * `fit` (:143-153); sigma (K,P) f64 in/out.  init != 0 (_initialize, :582-586): sigma = max(Re diag(F2 S F2^H), reg),

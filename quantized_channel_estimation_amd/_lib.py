@@ -39,6 +39,7 @@ SIGNATURES = {
                                       ctypes.c_int, ctypes.c_int, _vp]),
     "qce_model_set_option": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double]),
     "qce_estimate_assigned": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp]),
+    "qce_estimate_ls": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp]),
     "qce_prepare": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int, _vp, _vp,
                                    ctypes.c_int, _vp]),
     "qce_estimate": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, _vp, ctypes.c_int, _vp]),
@@ -245,15 +246,17 @@ class DeviceModel:
         check(load().qce_model_set_option(self._h, int(option), float(value)))
         self.M = 0
 
-    def estimate_assigned(self, y, comp=None):
-        """h_b = W_c y_b + b_c, c = comp[b] (None: c = b); host numpy I/O."""
+    def estimate_assigned(self, y, comp=None, ls=False):
+        """h_b = W_c y_b + b_c (ls: the least-squares solution with A_eff_c), c = comp[b] (None: c = b);
+        host numpy I/O."""
         y = np.ascontiguousarray(y, dtype=np.complex128)
         B = y.shape[0]
         if y.ndim != 2 or y.shape[1] != self.M:
             raise ValueError(f"y must be (B, {self.M})")
         c = None if comp is None else np.ascontiguousarray(comp, dtype=np.int64).reshape(B)
         out = np.empty((B, self.N), dtype=np.complex128)
-        check(load().qce_estimate_assigned(self._h, ptr(y), int(B), ptr(c), ptr(out), IO_HOST, None))
+        fn = load().qce_estimate_ls if ls else load().qce_estimate_assigned
+        check(fn(self._h, ptr(y), int(B), ptr(c), ptr(out), IO_HOST, None))
         return out
 
     def tables(self):

@@ -92,6 +92,71 @@ class BLMMSE:
         return out.astype(y.dtype, copy=False) if np.iscomplexobj(y) else out
 
 
+def _check_column_orthogonal(A):
+    if A is None:
+        return
+    A = np.asarray(A, dtype=complex)
+    G = A.conj().T @ A
+    if np.abs(G - np.diag(np.diag(G))).max() > 1e-12 * np.abs(np.diag(G)).max():
+        raise NotImplementedError("LS on the device needs a pilot matrix with orthogonal columns (I or kron(x, I))")
+
+
+class LS:
+    """Bussgang least squares (estimators/LS.py:15-76): h = lstsq(A_eff, y), A_eff = G A with the Bussgang
+    gain G of the global (estimate_global) or per-sample (estimate_genie) covariance."""
+
+    def __init__(self, snr, device=0, chunk=4096):
+        self.snr = snr
+        self.rho = 10 ** (0.1 * snr)
+        self.sigma2 = 1 / self.rho
+        self.device = device
+        self.chunk = int(chunk)
+
+    def _run(self, y, covs, A, n_bits, quantizer_type, quantizer, per_sample):
+        _check_column_orthogonal(A)
+        y = np.asarray(y)
+        est = BLMMSE(self.snr, device=self.device)
+        B = y.shape[0]
+        N = covs.shape[-1]
+        out = np.empty((B, N), dtype=np.complex128)
+        step = self.chunk if per_sample else max(B, 1)
+        for s in range(0, B, step):
+            e = min(B, s + step)
+            dm = est._model(covs[s:e] if per_sample else covs, A, n_bits, quantizer_type, quantizer)
+            try:
+                comp = None if per_sample else np.zeros(e - s, dtype=np.int64)
+                out[s:e] = dm.estimate_assigned(y[s:e], comp, ls=True)
+            finally:
+                dm.close()
+        return out
+
+    def estimate_global(self, y, C, A=None, n_bits=1, quantizer_type="uniform", quantizer=None):
+        """LS.py:55-76."""
+        y = np.asarray(y)
+        h = self._run(y, np.asarray(C, dtype=complex)[None], A, n_bits, quantizer_type, quantizer, False)
+        return h.astype(y.dtype, copy=False) if np.iscomplexobj(y) else h
+
+    def estimate_genie(self, y, t, A=None, n_bits=1, quantizer_type="uniform", quantizer=None):
+        """LS.py:21-53 (NaN rows -> 0, :48-52)."""
+        if n_bits == "inf" or n_bits == np.inf:
+            # LS.py:35-37 assigns lstsq's result tuple to a row, which numpy rejects
+            raise ValueError("setting an array element with a sequence.")
+        y = np.asarray(y)
+        h = self._run(y, _toeplitz_covs(t), A, n_bits, quantizer_type, quantizer, True)
+        h[np.isnan(h).any(axis=1)] = 0
+        return h.astype(y.dtype, copy=False) if np.iscomplexobj(y) else h
+
+
+def mp_LS_global(obj, *args):
+    """Bussgang_GMM.py:25-26."""
+    return obj.estimate_global(*args)
+
+
+def mp_LS_genie(obj, *args):
+    """Bussgang_GMM.py:22-23."""
+    return obj.estimate_genie(*args)
+
+
 def mp_eval(obj, y, toep, h_true, genie, A=None, n_bits=1, quantizer_type=None, quantizer=None, Cr=None):
     """blmmse.py:7-12 (the scripts' pool worker)."""
     if genie:

@@ -1226,8 +1226,21 @@ int qce_model_set_option(qce_model* m, int option, double value) {
   return fail(QCE_EARG, "unknown option");
 }
 
+static int assigned_impl(qce_model* m, const double* y, int64_t B, const int64_t* comp, double* h_out, int io,
+                         void* stream, int ls);
+
 int qce_estimate_assigned(qce_model* m, const double* y, int64_t B, const int64_t* comp, double* h_out, int io,
                           void* stream) {
+  return assigned_impl(m, y, B, comp, h_out, io, stream, 0);
+}
+
+int qce_estimate_ls(qce_model* m, const double* y, int64_t B, const int64_t* comp, double* h_out, int io,
+                    void* stream) {
+  return assigned_impl(m, y, B, comp, h_out, io, stream, 1);
+}
+
+static int assigned_impl(qce_model* m, const double* y, int64_t B, const int64_t* comp, double* h_out, int io,
+                         void* stream, int ls) {
   int rc = check_model(m, true);
   if (rc) return rc;
   if (B < 0 || (B > 0 && (!y || !h_out))) return fail(QCE_EARG, "bad arguments");
@@ -1254,7 +1267,8 @@ int qce_estimate_assigned(qce_model* m, const double* y, int64_t B, const int64_
       HIPCHK(sc.get(&p, sizeof(double2) * (size_t)B * m->N));
       dh = (double2*)p;
     }
-    HIPCHK(qce_launch_est_assigned(B, m->N, m->M, m->K, dy, dc, m->W.p, m->bvec.p, dh, st));
+    if (ls) HIPCHK(qce_launch_ls(B, m->N, m->M, dy, dc, m->Aeff.p, dh, st));
+    else HIPCHK(qce_launch_est_assigned(B, m->N, m->M, m->K, dy, dc, m->W.p, m->bvec.p, dh, st));
     if (io == QCE_IO_HOST)
       HIPCHK(hipMemcpyAsync(h_out, dh, sizeof(double2) * (size_t)B * m->N, hipMemcpyDeviceToHost, st));
   }

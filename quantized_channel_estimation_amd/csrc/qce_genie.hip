@@ -41,3 +41,37 @@ hipError_t qce_launch_est_assigned(long long B, int N, int M, int K, const doubl
   hipLaunchKernelGGL(k_est_assigned, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, N, M, y, comp, W, bvec, h);
   return hipGetLastError();
 }
+
+// Bussgang least squares for column-orthogonal effective matrices (estimators/LS.py: lstsq(A_eff, y) with
+// A_eff = G A, G diagonal, A = I or kron(x, I) as get_pilot_matrix builds it, so A_eff^H A_eff is diagonal):
+// h_i = sum_m conj(A_eff[m][i]) y_m / sum_m |A_eff[m][i]|^2, the minimum-norm least-squares solution.
+namespace {
+
+__global__ __launch_bounds__(256) void k_ls_colorth(long long B, int N, int M, const double2* __restrict__ y,
+                                                    const long long* __restrict__ comp,
+                                                    const double2* __restrict__ Aeff, double2* __restrict__ h) {
+  const long long b = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= B) return;
+  const long long c = comp ? comp[b] : b;
+  const double2* Ac = Aeff + c * (long long)M * N;
+  const double2* yb = y + b * M;
+  for (int i = lane; i < N; i += 64) {
+    double2 num = make_double2(0.0, 0.0);
+    double den = 0.0;
+    for (int m = 0; m < M; ++m) {
+      const double2 a = Ac[(long long)m * N + i];
+      num = cadd(num, cmul(cconj(a), yb[m]));
+      den += a.x * a.x + a.y * a.y;
+    }
+    h[b * N + i] = make_double2(num.x / den, num.y / den);
+  }
+}
+
+}  // namespace
+
+hipError_t qce_launch_ls(long long B, int N, int M, const double2* y, const long long* comp, const double2* Aeff,
+                         double2* h, hipStream_t st) {
+  hipLaunchKernelGGL(k_ls_colorth, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, N, M, y, comp, Aeff, h);
+  return hipGetLastError();
+}

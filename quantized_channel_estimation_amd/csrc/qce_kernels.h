@@ -233,3 +233,6 @@ int qce_rate_scratch();
 hipError_t qce_launch_rate(long long B, int N, const double2* he, const double2* h, const double* buss,
                            const double2* Cq, double clip, double2* inner, double* den2, double* part, double* stat,
                            hipStream_t st);
+// Bussgang LS with column-orthogonal A_eff (qce_genie.hip; estimators/LS.py)
+hipError_t qce_launch_ls(long long B, int N, int M, const double2* y, const long long* comp, const double2* Aeff,
+                         double2* h, hipStream_t st);

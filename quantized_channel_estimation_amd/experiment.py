@@ -4,7 +4,7 @@
 scripts' MSE and the statistical rate bound (rate.py).  Returns the script's (mse_list, rate_list) tables
 (rows = SNRs after the transpose of :313-314); writing CSV files is left to the caller.
 
-The LS branch (:166-200) is not provided; the rate bound needs the multi-bit get_Cr for n_bits in 2..8,
+The LS branch's per-sample ("genie") rate (:187-198) is not provided; the rate bound needs the multi-bit get_Cr for n_bits in 2..8,
 so rates are NaN there.
 """
 import copy
@@ -17,7 +17,7 @@ def run(n_antennas=64, n_components=64, n_summands_or_proba="all", n_path=1, n_b
         quantizer_type="uniform", snrs=(-10, -5, 0, 5, 10, 15, 20), n_train=100_000, n_val=10_000,
         zero_mean=True, blocks=None, seed=0, eval_rate=True, max_iter=100, device=0):
     from . import observe, rate
-    from .baselines import BLMMSE
+    from .baselines import BLMMSE, LS
     from .gmm import Gmm_nbit
     from .inputs import get_quantizer
     from .scm import SCMMulti
@@ -28,7 +28,7 @@ def run(n_antennas=64, n_components=64, n_summands_or_proba="all", n_path=1, n_b
     cov = h_train.T @ h_train.conj() / n_train  # sum of outer products / n_train (:119-123)
     quantizer = get_quantizer(list(snrs), n_bits, quantizer_type)
     rate_ok = eval_rate and (n_bits == 1 or np.isinf(n_bits))
-    mse = {k: [] for k in ("blmmse_glob", "blmmse_genie", "blmmse_gmm")}
+    mse = {k: [] for k in ("blmmse_glob", "LS_glob", "blmmse_genie", "blmmse_gmm")}
     rates = {k: [] for k in ("blmmse_glob_rstat", "blmmse_genie_rstat", "perfect_rstat", "gmm_rstat")}
     gmm = Gmm_nbit(n_components=n_components, covariance_type=cov_type, max_iter=max_iter, device=device)
     with warnings.catch_warnings():
@@ -39,6 +39,8 @@ def run(n_antennas=64, n_components=64, n_summands_or_proba="all", n_path=1, n_b
         r = observe.get_observation_nbit(h_val, snr, None, n_bits, thr, lab, seed=seed + 1 + i, device=device)
         est = BLMMSE(snr, device=device)
         res = {"blmmse_glob": est.estimate_global(r, cov, None, n_bits, quantizer_type, quantizer[snr]),
+               "LS_glob": LS(snr, device=device).estimate_global(r, cov, None, n_bits, quantizer_type,
+                                                                 quantizer[snr]),
                "blmmse_genie": est.estimate_genie(r, t_val, None, n_bits, quantizer_type, quantizer[snr]),
                "blmmse_gmm": copy.deepcopy(gmm).estimate_from_y(r, snr, n_antennas, None, n_summands_or_proba,
                                                                  n_bits, quantizer_type, quantizer[snr])}

@@ -4,7 +4,7 @@
 Runs ONLY in the build container (reference imported read-only, no bytecode written).  SCM channels
 with their Toeplitz first rows t (SCMMulti.generate_channel), a sample covariance as the global C
 (as Bussgang_GMM.py:131-139 builds it from training channels), fixed noise draws, and the reference's
-BLMMSE(snr).estimate_global / estimate_genie outputs for 1-bit, 2-bit uniform, 3-bit Lloyd-Max and
+BLMMSE(snr).estimate_global / estimate_genie and LS(snr) (estimators/LS.py) outputs for 1-bit, 2-bit uniform, 3-bit Lloyd-Max and
 n_bits = inf, with A = I and a 2-pilot A.
 
 Usage:  python -B tests/golden/make_golden_baselines.py
@@ -24,6 +24,7 @@ def main():
     ut = R["ut"]
     sys.path.insert(0, "/root/reference")
     from estimators.blmmse import BLMMSE
+    from estimators.LS import LS
     warnings.simplefilter("ignore")
     N = 16
     scm = R["SCMMulti"](path_sigma=2.0, n_path=3)
@@ -56,6 +57,10 @@ def main():
             out[p + "thr"], out[p + "lab"] = np.asarray(quantizer[0]), np.asarray(quantizer[1])
         out[p + "h_global"] = est.estimate_global(y, C, A, nb, qt, quantizer)
         out[p + "h_genie"] = est.estimate_genie(y, t, A, nb, qt, quantizer)
+        ls = LS(snr)
+        out[p + "ls_global"] = ls.estimate_global(y, C, A, nb, qt, quantizer)
+        if nb != np.inf:  # the reference's genie LS assigns lstsq's tuple for n_bits = inf (LS.py:35-37) and fails
+            out[p + "ls_genie"] = ls.estimate_genie(y, t, A, nb, qt, quantizer)
         tags.append(tag)
     out["tags"] = np.array(tags)
     np.savez_compressed(os.path.join(HERE, "baselines.npz"), **out)

@@ -62,3 +62,17 @@ def test_gpu_blmmse_matches_reference(bl, tag):
     assert rel_fro(hg, bl[tag + "__h_global"]) < 1e-5, tag
     hq = mp_eval(est, y, bl["t"], None, True, A, nb, qt, quantizer)
     assert rel_fro(hq, bl[tag + "__h_genie"]) < 1e-5, tag
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", TAGS)
+def test_gpu_ls_matches_reference(bl, tag):
+    from quantized_channel_estimation_amd.baselines import LS
+    y, snr, nb, qt, quantizer, A = _case(bl, tag)
+    ls = LS(snr, chunk=50)
+    assert rel_fro(ls.estimate_global(y, bl["C"], A, nb, qt, quantizer), bl[tag + "__ls_global"]) < 1e-9, tag
+    if (tag + "__ls_genie") in bl:
+        assert rel_fro(ls.estimate_genie(y, bl["t"], A, nb, qt, quantizer), bl[tag + "__ls_genie"]) < 1e-9, tag
+    else:
+        with pytest.raises(ValueError):
+            ls.estimate_genie(y, bl["t"], A, nb, qt, quantizer)
