@@ -27,7 +27,7 @@ def run(n_antennas=64, n_components=64, n_summands_or_proba="all", n_path=1, n_b
     h_train, h_val, t_val = h_all[:n_train], h_all[n_train:], t_all[n_train:]
     cov = h_train.T @ h_train.conj() / n_train  # sum of outer products / n_train (:119-123)
     quantizer = get_quantizer(list(snrs), n_bits, quantizer_type)
-    rate_ok = eval_rate and (n_bits == 1 or np.isinf(n_bits))
+    rate_ok = eval_rate
     mse = {k: [] for k in ("blmmse_glob", "LS_glob", "blmmse_genie", "blmmse_gmm")}
     rates = {k: [] for k in ("blmmse_glob_rstat", "blmmse_genie_rstat", "perfect_rstat", "gmm_rstat")}
     gmm = Gmm_nbit(n_components=n_components, covariance_type=cov_type, max_iter=max_iter, device=device)
@@ -47,7 +47,7 @@ def run(n_antennas=64, n_components=64, n_summands_or_proba="all", n_path=1, n_b
         for k, v in res.items():
             mse[k].append(observe.mse(v, h_val, device=device))
         if rate_ok:
-            g, Cq = rate.bussgang_global(cov, snr, n_bits, device=device)
+            g, Cq, _ = rate.bussgang_global(cov, snr, n_bits, quantizer[snr], device=device)
             rates["blmmse_glob_rstat"].append(rate.statistical_rate_bound(res["blmmse_glob"], h_val, g, Cq))
             rates["blmmse_genie_rstat"].append(rate.statistical_rate_bound(res["blmmse_genie"], h_val, g, Cq))
             rates["perfect_rstat"].append(rate.statistical_rate_bound(h_val, h_val, g, Cq))

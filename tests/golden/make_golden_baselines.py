@@ -63,6 +63,14 @@ def main():
             out[p + "ls_genie"] = ls.estimate_genie(y, t, A, nb, qt, quantizer)
         tags.append(tag)
     out["tags"] = np.array(tags)
+    # the scripts' Bussgang pair for the rate bound (Bussgang_GMM.py:148-151): uniform get_Bussgang_matrix
+    # and get_Cr (quantised-variance diagonal, uniform_quantizer.py:114-173) for multi-bit quantisers
+    from modules.uniform_quantizer import get_Bussgang_matrix, get_Cr
+    for tag, snr, nb, qt in [("r2u", 5.0, 2, "uniform"), ("r3l", 0.0, 3, "lloyd"), ("r1", 5.0, 1, "uniform")]:
+        quantizer = ut.get_quantizer([snr], nb, qt)[snr]
+        Cy = C + 10 ** (-snr / 10) * np.eye(N, dtype=complex)
+        out[tag + "__buss"] = np.real(np.diag(get_Bussgang_matrix(snr, nb, Cy)))
+        out[tag + "__Cr"] = get_Cr(Cy, nb, snr, quantizer)
     np.savez_compressed(os.path.join(HERE, "baselines.npz"), **out)
     print("wrote baselines.npz:", tags)
 

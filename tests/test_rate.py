@@ -34,7 +34,7 @@ def test_gpu_rate_bound_vs_oracle(n_bits, clip):
     from oracle import qce_oracle as O
     from quantized_channel_estimation_amd import rate
     h, he, cov = _data()
-    g, Cq = rate.bussgang_global(cov, 5.0, n_bits)
+    g, Cq, _ = rate.bussgang_global(cov, 5.0, n_bits)
     # the pair the scripts build (uniform_quantizer.get_Bussgang_matrix / get_Cr), restated
     Cy = cov + 10 ** (-5.0 / 10) * np.eye(32)
     if n_bits == 1:
@@ -53,3 +53,29 @@ def test_gpu_rate_bound_vs_oracle(n_bits, clip):
     assert abs(terms["den2"] - den2) <= 1e-11 * den2
     rd = rate.statistical_rate_bound(torch.from_numpy(he).cuda(), torch.from_numpy(h).cuda(), g, Cq, norm_clip=clip)
     assert abs(rd - r) <= 1e-13 * abs(r)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag,snr,nb,qt", [("r2u", 5.0, 2, "uniform"), ("r3l", 0.0, 3, "lloyd"), ("r1", 5.0, 1, "uniform")])
+def test_gpu_bussgang_pair_matches_reference(tag, snr, nb, qt):
+    """get_Bussgang_matrix / get_Cr of the reference (tests/golden/baselines.npz) for the rate bound."""
+    import os
+    from conftest import GOLDEN
+    from quantized_channel_estimation_amd import inputs, rate
+    bl = np.load(os.path.join(GOLDEN, "baselines.npz"), allow_pickle=False)
+    quantizer = inputs.get_quantizer([snr], nb, qt)[snr]
+    g, Cq, Cr = rate.bussgang_global(bl["C"], snr, nb, quantizer)
+    assert np.abs(g - bl[tag + "__buss"]).max() <= 1e-13 * np.abs(g).max()
+    assert np.abs(Cr - bl[tag + "__Cr"]).max() <= 1e-11 * np.abs(Cr).max()
+
+
+def test_quantized_variance_matches_reference():
+    import os
+    from conftest import GOLDEN
+    from quantized_channel_estimation_amd import inputs, rate
+    bl = np.load(os.path.join(GOLDEN, "baselines.npz"), allow_pickle=False)
+    for tag, snr, nb, qt in [("r2u", 5.0, 2, "uniform"), ("r3l", 0.0, 3, "lloyd")]:
+        quantizer = inputs.get_quantizer([snr], nb, qt)[snr]
+        d = np.real(np.diag(bl["C"])) + 10 ** (-snr / 10)
+        assert np.allclose(rate.quantized_variance(d, quantizer[0], quantizer[1]), np.real(np.diag(bl[tag + "__Cr"])),
+                           rtol=1e-12, atol=0)
