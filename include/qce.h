@@ -158,6 +158,12 @@ int qce_estimate_assigned(qce_model* model, const double* y, int64_t B, const in
 int qce_estimate_ls(qce_model* model, const double* y, int64_t B, const int64_t* comp, double* h_out, int io,
                     void* stream);
 
+/* Bussgang least squares for a general pilot matrix with full column rank (M >= N): h_b = pinv(A_eff_c) y_b,
+ * the same solution as estimators/LS.py:32,47,73 (np.linalg.lstsq(A_eff, y)) for full-rank A_eff.  The
+ * pseudo-inverses are formed on the device per call (normal equations, Gauss-Jordan).  M < N -> QCE_ENOTIMPL. */
+int qce_estimate_ls_general(qce_model* model, const double* y, int64_t B, const int64_t* comp, double* h_out,
+                            int io, void* stream);
+
 /* Toeplitz / block-Toeplitz inverse-EM covariance step (gmm_cplx_bussgang.py:792-826, Barton & Fuhrmann):
  * S (K,N,N) c128 = the M-step's weighted sample covariances WITHOUT reg; F2 (P,N) c128 the partial DFT of
  * `fit` (:143-153); sigma (K,P) f64 in/out.  init != 0 (_initialize, :582-586): sigma = max(Re diag(F2 S F2^H), reg),

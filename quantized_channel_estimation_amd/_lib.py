@@ -40,6 +40,7 @@ SIGNATURES = {
     "qce_model_set_option": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double]),
     "qce_estimate_assigned": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp]),
     "qce_estimate_ls": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp]),
+    "qce_estimate_ls_general": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp]),
     "qce_prepare": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int, _vp, _vp,
                                    ctypes.c_int, _vp]),
     "qce_estimate": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, _vp, ctypes.c_int, _vp]),
@@ -247,7 +248,8 @@ class DeviceModel:
         self.M = 0
 
     def estimate_assigned(self, y, comp=None, ls=False):
-        """h_b = W_c y_b + b_c (ls: the least-squares solution with A_eff_c), c = comp[b] (None: c = b);
+        """h_b = W_c y_b + b_c (ls: the least-squares solution with A_eff_c; ls="general": full-column-rank A_eff_c, not only
+        column-orthogonal ones), c = comp[b] (None: c = b);
         host numpy I/O."""
         y = np.ascontiguousarray(y, dtype=np.complex128)
         B = y.shape[0]
@@ -255,7 +257,10 @@ class DeviceModel:
             raise ValueError(f"y must be (B, {self.M})")
         c = None if comp is None else np.ascontiguousarray(comp, dtype=np.int64).reshape(B)
         out = np.empty((B, self.N), dtype=np.complex128)
-        fn = load().qce_estimate_ls if ls else load().qce_estimate_assigned
+        if ls == "general":
+            fn = load().qce_estimate_ls_general
+        else:
+            fn = load().qce_estimate_ls if ls else load().qce_estimate_assigned
         check(fn(self._h, ptr(y), int(B), ptr(c), ptr(out), IO_HOST, None))
         return out
 

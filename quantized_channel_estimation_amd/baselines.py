@@ -92,13 +92,18 @@ class BLMMSE:
         return out.astype(y.dtype, copy=False) if np.iscomplexobj(y) else out
 
 
-def _check_column_orthogonal(A):
+def _ls_kind(A):
+    """True for column-orthogonal A (I or kron(x, I): the per-column kernel), "general" for any other A with
+    at least as many rows as columns (device pseudo-inverse)."""
     if A is None:
-        return
+        return True
     A = np.asarray(A, dtype=complex)
     G = A.conj().T @ A
-    if np.abs(G - np.diag(np.diag(G))).max() > 1e-12 * np.abs(np.diag(G)).max():
-        raise NotImplementedError("LS on the device needs a pilot matrix with orthogonal columns (I or kron(x, I))")
+    if np.abs(G - np.diag(np.diag(G))).max() <= 1e-12 * np.abs(np.diag(G)).max():
+        return True
+    if A.shape[0] < A.shape[1]:
+        raise NotImplementedError("LS on the device needs column-orthogonal A or A with M >= N")
+    return "general"
 
 
 class LS:
@@ -113,7 +118,7 @@ class LS:
         self.chunk = int(chunk)
 
     def _run(self, y, covs, A, n_bits, quantizer_type, quantizer, per_sample):
-        _check_column_orthogonal(A)
+        kind = _ls_kind(A)
         y = np.asarray(y)
         est = BLMMSE(self.snr, device=self.device)
         B = y.shape[0]
@@ -125,7 +130,7 @@ class LS:
             dm = est._model(covs[s:e] if per_sample else covs, A, n_bits, quantizer_type, quantizer)
             try:
                 comp = None if per_sample else np.zeros(e - s, dtype=np.int64)
-                out[s:e] = dm.estimate_assigned(y[s:e], comp, ls=True)
+                out[s:e] = dm.estimate_assigned(y[s:e], comp, ls=kind)
             finally:
                 dm.close()
         return out

@@ -1239,6 +1239,14 @@ int qce_estimate_ls(qce_model* m, const double* y, int64_t B, const int64_t* com
   return assigned_impl(m, y, B, comp, h_out, io, stream, 1);
 }
 
+int qce_estimate_ls_general(qce_model* m, const double* y, int64_t B, const int64_t* comp, double* h_out, int io,
+                            void* stream) {
+  int rc = check_model(m, true);
+  if (rc) return rc;
+  if (m->M < m->N) return fail(QCE_ENOTIMPL, "general LS needs M >= N (full column rank A_eff)");
+  return assigned_impl(m, y, B, comp, h_out, io, stream, 2);
+}
+
 static int assigned_impl(qce_model* m, const double* y, int64_t B, const int64_t* comp, double* h_out, int io,
                          void* stream, int ls) {
   int rc = check_model(m, true);
@@ -1267,7 +1275,14 @@ static int assigned_impl(qce_model* m, const double* y, int64_t B, const int64_t
       HIPCHK(sc.get(&p, sizeof(double2) * (size_t)B * m->N));
       dh = (double2*)p;
     }
-    if (ls) HIPCHK(qce_launch_ls(B, m->N, m->M, dy, dc, m->Aeff.p, dh, st));
+    if (ls == 2) {
+      void *T, *P, *bz;
+      HIPCHK(sc.get(&T, sizeof(double2) * (size_t)m->K * m->N * (m->N + m->M)));
+      HIPCHK(sc.get(&P, sizeof(double2) * (size_t)m->K * m->N * m->M));
+      HIPCHK(sc.get(&bz, sizeof(double2) * (size_t)m->K * m->N));
+      HIPCHK(qce_launch_ls_pinv(m->K, m->N, m->M, m->Aeff.p, (double2*)T, (double2*)P, (double2*)bz, st));
+      HIPCHK(qce_launch_est_assigned(B, m->N, m->M, m->K, dy, dc, (const double2*)P, (const double2*)bz, dh, st));
+    } else if (ls) HIPCHK(qce_launch_ls(B, m->N, m->M, dy, dc, m->Aeff.p, dh, st));
     else HIPCHK(qce_launch_est_assigned(B, m->N, m->M, m->K, dy, dc, m->W.p, m->bvec.p, dh, st));
     if (io == QCE_IO_HOST)
       HIPCHK(hipMemcpyAsync(h_out, dh, sizeof(double2) * (size_t)B * m->N, hipMemcpyDeviceToHost, st));

@@ -75,3 +75,61 @@ hipError_t qce_launch_ls(long long B, int N, int M, const double2* y, const long
   hipLaunchKernelGGL(k_ls_colorth, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, N, M, y, comp, Aeff, h);
   return hipGetLastError();
 }
+
+// Bussgang least squares for a general full-column-rank effective matrix (estimators/LS.py:32,47,73:
+// lstsq(A_eff, y), M >= N): per component c the pseudo-inverse P_c = (A_eff^H A_eff)^{-1} A_eff^H is formed
+// once by Gauss-Jordan elimination of the Hermitian positive-definite Gram matrix (no pivoting needed) on the
+// augmented N x (N + M) tableau [G | A_eff^H] held in device scratch; h_b = P_c y_b then runs on
+// k_est_assigned with a zero offset.  One workgroup per component; the tableau is O(K N (N + M)) bytes.
+namespace {
+
+__global__ __launch_bounds__(256) void k_ls_pinv(int N, int M, const double2* __restrict__ Aeff,
+                                                 double2* __restrict__ T, double2* __restrict__ P,
+                                                 double2* __restrict__ bzero) {
+  __shared__ double2 f[256];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const int L = N + M;
+  const double2* A = Aeff + (long long)c * M * N;  // (M, N) row-major
+  double2* Tc = T + (long long)c * N * L;
+  for (int idx = tid; idx < N * L; idx += 256) {
+    const int i = idx / L, j = idx % L;
+    double2 v = make_double2(0.0, 0.0);
+    if (j < N) {
+      for (int m = 0; m < M; ++m) v = cadd(v, cmul(cconj(A[(long long)m * N + i]), A[(long long)m * N + j]));
+    } else {
+      v = cconj(A[(long long)(j - N) * N + i]);
+    }
+    Tc[idx] = v;
+  }
+  for (int i = tid; i < N; i += 256) bzero[(long long)c * N + i] = make_double2(0.0, 0.0);
+  __syncthreads();
+  for (int p = 0; p < N; ++p) {
+    const double2 piv = Tc[(long long)p * L + p];
+    const double ip = 1.0 / (piv.x * piv.x + piv.y * piv.y);
+    const double2 inv = make_double2(piv.x * ip, -piv.y * ip);
+    for (int r = tid; r < N; r += 256) f[r] = cmul(Tc[(long long)r * L + p], inv);
+    __syncthreads();
+    for (int idx = tid; idx < N * (L - p); idx += 256) {
+      const int r = idx / (L - p), j = p + idx % (L - p);
+      if (r == p) continue;
+      Tc[(long long)r * L + j] = cadd(Tc[(long long)r * L + j], cmul(make_double2(-f[r].x, -f[r].y), Tc[(long long)p * L + j]));
+    }
+    __syncthreads();
+    for (int j = p + tid; j < L; j += 256) Tc[(long long)p * L + j] = cmul(Tc[(long long)p * L + j], inv);
+    __syncthreads();
+  }
+  double2* Pc = P + (long long)c * N * M;
+  for (int idx = tid; idx < N * M; idx += 256) {
+    const int i = idx / M, m = idx % M;
+    Pc[idx] = Tc[(long long)i * L + N + m];
+  }
+}
+
+}  // namespace
+
+hipError_t qce_launch_ls_pinv(int K, int N, int M, const double2* Aeff, double2* T, double2* P, double2* bzero,
+                              hipStream_t st) {
+  if (N > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_ls_pinv, dim3((unsigned)K), dim3(256), 0, st, N, M, Aeff, T, P, bzero);
+  return hipGetLastError();
+}

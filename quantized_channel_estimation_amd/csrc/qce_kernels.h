@@ -236,3 +236,6 @@ hipError_t qce_launch_rate(long long B, int N, const double2* he, const double2*
 // Bussgang LS with column-orthogonal A_eff (qce_genie.hip; estimators/LS.py)
 hipError_t qce_launch_ls(long long B, int N, int M, const double2* y, const long long* comp, const double2* Aeff,
                          double2* h, hipStream_t st);
+// Pseudo-inverses P_c = (A_eff^H A_eff)^{-1} A_eff^H of full-column-rank A_eff (qce_genie.hip; LS.py general A)
+hipError_t qce_launch_ls_pinv(int K, int N, int M, const double2* Aeff, double2* T, double2* P, double2* bzero,
+                              hipStream_t st);

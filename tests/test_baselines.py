@@ -76,3 +76,49 @@ def test_gpu_ls_matches_reference(bl, tag):
     else:
         with pytest.raises(ValueError):
             ls.estimate_genie(y, bl["t"], A, nb, qt, quantizer)
+
+
+def _ls_general_expected(y, covs, A, snr, n_bits):
+    """LS.py:21-32 / :55-73 restated for the test: A_eff = sqrt(2/pi) diag(Cy)^-1/2 A (1-bit) or A (inf),
+    h = lstsq(A_eff, y) per covariance."""
+    out = []
+    for C, yb in zip(covs, y):
+        Cy = A @ C @ A.conj().T + 10 ** (-0.1 * snr) * np.eye(A.shape[0])
+        Ae = A if n_bits == np.inf else np.sqrt(2 / np.pi) * np.diag(1 / np.sqrt(np.real(np.diag(Cy)))) @ A
+        out.append(np.linalg.lstsq(Ae, yb.T, rcond=None)[0].T)
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_bits", [1, np.inf])
+def test_gpu_ls_general_pilot_matrix(bl, n_bits):
+    """LS with a dense, non-column-orthogonal pilot matrix (M = 2N rows): device pseudo-inverse vs lstsq."""
+    from quantized_channel_estimation_amd.baselines import LS, _toeplitz_covs
+    rng = np.random.default_rng(7)
+    C = bl["C"]
+    N = C.shape[0]
+    M = 2 * N
+    A = (rng.standard_normal((M, N)) + 1j * rng.standard_normal((M, N))) / np.sqrt(2 * M)
+    B = 40
+    y = (np.sign(rng.standard_normal((B, M))) + 1j * np.sign(rng.standard_normal((B, M)))) / np.sqrt(2)
+    snr = 5.0
+    ls = LS(snr, chunk=16)
+    hg = ls.estimate_global(y, C, A, n_bits)
+    exp_g = _ls_general_expected([y], [C], A, snr, n_bits)[0]
+    assert rel_fro(hg, exp_g) < 1e-9
+    if n_bits == 1:
+        t = bl["t"][:B]
+        covs = _toeplitz_covs(t)
+        hq = ls.estimate_genie(y, t, A, n_bits)
+        exp_q = np.stack([_ls_general_expected([y[b:b + 1]], [covs[b]], A, snr, n_bits)[0][0] for b in range(B)])
+        assert rel_fro(hq, exp_q) < 1e-9
+
+
+def test_ls_kind_routes_pilot_matrices():
+    from quantized_channel_estimation_amd.baselines import _ls_kind
+    assert _ls_kind(None) is True
+    assert _ls_kind(np.kron(np.array([[1.0], [1j]]), np.eye(4))) is True
+    rng = np.random.default_rng(0)
+    assert _ls_kind(rng.standard_normal((8, 4)) + 0j) == "general"
+    with pytest.raises(NotImplementedError):
+        _ls_kind(rng.standard_normal((3, 4)) + 0j)
