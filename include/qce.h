@@ -191,6 +191,13 @@ int qce_scm_generate(int64_t B, int n_coherence, int N, int n_path, double path_
 int qce_rate_bound(const double* h_est, const double* h, int64_t B, int N, const double* buss, const double* Cq,
                    double norm_clip, double* out, int device, int io, void* stream);
 
+/* Per-sample matched-filter rate of the scripts' LS branch (Bussgang_GMM.py:186-198): g = (buss o h_est_b)^H Cq^-1,
+ * out[0] = mean_b Re log2(1 + |g B h_est_b|^2 / (g Cq g^H + |g B (h_b - h_est_b)|^2)), B = diag(buss).  Cq^-1 is
+ * formed on the device (Cq Hermitian, full rank: equal to np.linalg.pinv to rounding).  h_est / h (B,N) c128
+ * where `io` says; buss (N,) f64, Cq (N,N) c128 and out host; N <= 256; synchronous. */
+int qce_rate_mf(const double* h_est, const double* h, int64_t B, int N, const double* buss, const double* Cq,
+                double* out, int device, int io, void* stream);
+
 /* Device synchronisation of the model's stream (for timing and for QCE_IO_DEVICE callers). */
 int qce_synchronize(qce_model* model);
 

@@ -35,6 +35,8 @@ SIGNATURES = {
                                        ctypes.c_int, _vp, ctypes.c_int, _vp]),
     "qce_scm_generate": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double, _vp,
                                         _vp, _vp, ctypes.c_uint64, _vp, _vp, ctypes.c_int, ctypes.c_int, _vp]),
+    "qce_rate_mf": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int,
+                                   _vp]),
     "qce_rate_bound": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, _vp, _vp, ctypes.c_double, _vp,
                                       ctypes.c_int, ctypes.c_int, _vp]),
     "qce_model_set_option": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_double]),

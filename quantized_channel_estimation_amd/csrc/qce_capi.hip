@@ -1428,6 +1428,42 @@ int qce_rate_bound(const double* h_est, const double* h, int64_t B, int N, const
   return QCE_OK;
 }
 
+int qce_rate_mf(const double* h_est, const double* h, int64_t B, int N, const double* buss, const double* Cq,
+                double* out, int device, int io, void* stream) {
+  if (B < 1 || N < 1 || N > 256 || !h_est || !h || !buss || !Cq || !out) return fail(QCE_EARG, "rate_mf: bad arguments");
+  if (io != QCE_IO_HOST && io != QCE_IO_DEVICE) return fail(QCE_EARG, "rate_mf: bad io");
+  DeviceGuard g(device);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t nb = (size_t)B * N, nn = (size_t)N * N;
+  {
+    StreamScratch sc(st);
+    void *dhe = (void*)h_est, *dh = (void*)h, *dbuss, *dcq, *T, *cqi, *bz, *rate, *sum;
+    HIPCHK(sc.get(&dbuss, sizeof(double) * N));
+    HIPCHK(sc.get(&dcq, sizeof(double2) * nn));
+    HIPCHK(sc.get(&T, sizeof(double2) * nn * 2));
+    HIPCHK(sc.get(&cqi, sizeof(double2) * nn));
+    HIPCHK(sc.get(&bz, sizeof(double2) * N));
+    HIPCHK(sc.get(&rate, sizeof(double) * (size_t)B));
+    HIPCHK(sc.get(&sum, sizeof(double)));
+    HIPCHK(hipMemcpyAsync(dbuss, buss, sizeof(double) * N, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dcq, Cq, sizeof(double2) * nn, hipMemcpyHostToDevice, st));
+    if (io == QCE_IO_HOST) {
+      HIPCHK(sc.get(&dhe, sizeof(double2) * nb));
+      HIPCHK(sc.get(&dh, sizeof(double2) * nb));
+      HIPCHK(hipMemcpyAsync(dhe, h_est, sizeof(double2) * nb, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(dh, h, sizeof(double2) * nb, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(qce_launch_ls_pinv(1, N, N, (const double2*)dcq, (double2*)T, (double2*)cqi, (double2*)bz, st));
+    HIPCHK(qce_launch_rate_mf(B, N, (const double2*)dhe, (const double2*)dh, (const double*)dbuss, (const double2*)dcq,
+                              (const double2*)cqi, (double*)rate, (double*)sum, st));
+    double r = 0.0;
+    HIPCHK(hipMemcpyAsync(&r, sum, sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    out[0] = r / (double)B;
+  }
+  return QCE_OK;
+}
+
 int qce_synchronize(qce_model* m) {
   if (!m) return fail(QCE_EARG, "null model");
   DeviceGuard g(m->device);

@@ -133,3 +133,83 @@ hipError_t qce_launch_ls_pinv(int K, int N, int M, const double2* Aeff, double2*
   hipLaunchKernelGGL(k_ls_pinv, dim3((unsigned)K), dim3(256), 0, st, N, M, Aeff, T, P, bzero);
   return hipGetLastError();
 }
+
+// Per-sample matched-filter rate of the scripts' LS branch (Bussgang_GMM.py:186-198): with v = B h_est_b,
+// e = B (h_b - h_est_b), B = diag(buss) and g = v^H Cq^-1:
+// rate_b = Re log2(1 + |g v|^2 / (g Cq g^H + |g e|^2)).  One wave per sample; Cq^-1 from k_ls_pinv.
+namespace {
+
+__global__ __launch_bounds__(256) void k_rate_mf(long long B, int N, const double2* __restrict__ he,
+                                                 const double2* __restrict__ h, const double* __restrict__ buss,
+                                                 const double2* __restrict__ Cq, const double2* __restrict__ Cqi,
+                                                 double* __restrict__ rate) {
+  __shared__ double2 vs[4][256], gs[4][256];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long b = (long long)blockIdx.x * 4 + w;
+  if (b >= B) return;  // no block-wide barrier below: each wave works on its own LDS rows
+  double2 ev[4];
+  for (int q = 0; q < 4; ++q) {
+    const int i = lane + 64 * q;
+    if (i < N) {
+      const double2 r = he[b * N + i], t = h[b * N + i];
+      vs[w][i] = make_double2(buss[i] * r.x, buss[i] * r.y);
+      ev[q] = make_double2(buss[i] * (t.x - r.x), buss[i] * (t.y - r.y));
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  for (int q = 0; q < 4; ++q) {
+    const int j = lane + 64 * q;
+    if (j < N) {
+      double2 g = make_double2(0.0, 0.0);
+      for (int i = 0; i < N; ++i) g = cadd(g, cmul(cconj(vs[w][i]), Cqi[(long long)i * N + j]));
+      gs[w][j] = g;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  double s[6] = {0, 0, 0, 0, 0, 0};
+  for (int q = 0; q < 4; ++q) {
+    const int j = lane + 64 * q;
+    if (j < N) {
+      const double2 g = gs[w][j];
+      const double2 a = cmul(g, vs[w][j]), c = cmul(g, ev[q]);
+      double2 t = make_double2(0.0, 0.0);
+      for (int k = 0; k < N; ++k) t = cadd(t, cmul(Cq[(long long)j * N + k], cconj(gs[w][k])));
+      const double2 d = cmul(g, t);
+      s[0] += a.x; s[1] += a.y; s[2] += d.x; s[3] += d.y; s[4] += c.x; s[5] += c.y;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1)
+    for (int u = 0; u < 6; ++u) s[u] += __shfl_xor(s[u], o, 64);
+  if (lane == 0) {
+    const double num = s[0] * s[0] + s[1] * s[1];
+    const double dr = s[2] + s[4] * s[4] + s[5] * s[5], di = s[3];
+    const double dd = dr * dr + di * di;
+    const double zr = 1.0 + num * dr / dd, zi = -num * di / dd;
+    rate[b] = log2(sqrt(zr * zr + zi * zi));
+  }
+}
+
+__global__ __launch_bounds__(256) void k_sum_fixed(long long B, const double* __restrict__ x, double* __restrict__ out) {
+  __shared__ double p[256];
+  double acc = 0.0;
+  for (long long i = threadIdx.x; i < B; i += 256) acc += x[i];
+  p[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) p[threadIdx.x] += p[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = p[0];
+}
+
+}  // namespace
+
+hipError_t qce_launch_rate_mf(long long B, int N, const double2* he, const double2* h, const double* buss,
+                              const double2* Cq, const double2* Cqi, double* rate, double* sum, hipStream_t st) {
+  if (N > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_rate_mf, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, N, he, h, buss, Cq, Cqi, rate);
+  hipLaunchKernelGGL(k_sum_fixed, dim3(1), dim3(256), 0, st, B, rate, sum);
+  return hipGetLastError();
+}

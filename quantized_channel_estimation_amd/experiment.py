@@ -4,8 +4,9 @@
 scripts' MSE and the statistical rate bound (rate.py).  Returns the script's (mse_list, rate_list) tables
 (rows = SNRs after the transpose of :313-314); writing CSV files is left to the caller.
 
-The LS branch's per-sample ("genie") rate (:187-198) is not provided; the rate bound needs the multi-bit get_Cr for n_bits in 2..8,
-so rates are NaN there.
+The LS branch's per-sample matched-filter rate (:186-198, rate.matched_filter_rate) is its own column
+"LS_glob_mf" (the script appends it to the previous method's rate row, rate_list[-2]); its statistical bound
+(:200-211) is "LS_glob_stat".
 """
 import copy
 import warnings
@@ -29,7 +30,8 @@ def run(n_antennas=64, n_components=64, n_summands_or_proba="all", n_path=1, n_b
     quantizer = get_quantizer(list(snrs), n_bits, quantizer_type)
     rate_ok = eval_rate
     mse = {k: [] for k in ("blmmse_glob", "LS_glob", "blmmse_genie", "blmmse_gmm")}
-    rates = {k: [] for k in ("blmmse_glob_rstat", "blmmse_genie_rstat", "perfect_rstat", "gmm_rstat")}
+    rates = {k: [] for k in ("blmmse_glob_rstat", "blmmse_genie_rstat", "perfect_rstat", "gmm_rstat",
+                         "LS_glob_mf", "LS_glob_stat")}
     gmm = Gmm_nbit(n_components=n_components, covariance_type=cov_type, max_iter=max_iter, device=device)
     with warnings.catch_warnings():
         warnings.simplefilter("ignore")
@@ -52,6 +54,8 @@ def run(n_antennas=64, n_components=64, n_summands_or_proba="all", n_path=1, n_b
             rates["blmmse_genie_rstat"].append(rate.statistical_rate_bound(res["blmmse_genie"], h_val, g, Cq))
             rates["perfect_rstat"].append(rate.statistical_rate_bound(h_val, h_val, g, Cq))
             rates["gmm_rstat"].append(rate.statistical_rate_bound(res["blmmse_gmm"], h_val, g, Cq, norm_clip=1e-1))
+            rates["LS_glob_mf"].append(rate.matched_filter_rate(res["LS_glob"], h_val, g, Cq, device=device))
+            rates["LS_glob_stat"].append(rate.statistical_rate_bound(res["LS_glob"], h_val, g, Cq))
         else:
             for k in rates:
                 rates[k].append(float("nan"))

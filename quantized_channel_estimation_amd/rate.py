@@ -37,6 +37,20 @@ def statistical_rate_bound(h_est, h, buss, Cq, norm_clip=None, device=0, return_
     return float(out[0])
 
 
+def matched_filter_rate(h_est, h, buss, Cq, device=0):
+    """Per-sample matched-filter rate of the LS branch (Bussgang_GMM.py:186-198), averaged over samples:
+    g = h_est_b^H B^H Cq^-1, Re log2(1 + |g B h_est_b|^2 / (g Cq g^H + |g B (h_b - h_est_b)|^2))."""
+    buss = np.ascontiguousarray(np.real(np.diag(buss)) if np.ndim(buss) == 2 else np.real(buss), dtype=np.float64)
+    Cq = np.ascontiguousarray(Cq, dtype=np.complex128)
+    a = np.ascontiguousarray(h_est, dtype=np.complex128)
+    b = np.ascontiguousarray(h, dtype=np.complex128)
+    B, N = a.shape
+    out = np.zeros(1)
+    _lib.check(_lib.load().qce_rate_mf(_lib.ptr(a), _lib.ptr(b), B, N, _lib.ptr(buss), _lib.ptr(Cq), _lib.ptr(out),
+                                       int(device), _lib.IO_HOST, None))
+    return float(out[0])
+
+
 def quantized_variance(d, thresholds, labels):
     """get_quantized_variance (uniform_quantizer.py:114-128): output variance of the per-component
     quantiser for complex inputs of variance d."""

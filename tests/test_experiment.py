@@ -18,3 +18,4 @@ def test_gpu_experiment_end_to_end():
     r = np.array([row[1:] for row in rates[1:]], dtype=float)
     assert np.isfinite(r).all()
     assert (r[:, 2] >= r[:, 0]).all()  # perfect CSI bound above the global estimate's
+    assert rates[0][5:] == ["LS_glob_mf", "LS_glob_stat"]

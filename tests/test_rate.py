@@ -79,3 +79,26 @@ def test_quantized_variance_matches_reference():
         d = np.real(np.diag(bl["C"])) + 10 ** (-snr / 10)
         assert np.allclose(rate.quantized_variance(d, quantizer[0], quantizer[1]), np.real(np.diag(bl[tag + "__Cr"])),
                            rtol=1e-12, atol=0)
+
+
+def test_oracle_mf_rate_is_finite_and_ordered():
+    from oracle import qce_oracle as O
+    h, he, cov = _data(B=200)
+    g = np.full(32, 0.5)
+    Cq = 0.1 * np.eye(32) + 0.02 * cov
+    r_est = O.rate_mf(he, h, g, Cq)
+    r_perfect = O.rate_mf(h, h, g, Cq)
+    assert np.isfinite(r_est) and r_perfect > r_est
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_bits", [1, np.inf])
+def test_gpu_mf_rate_vs_oracle(n_bits):
+    """LS branch per-sample rate (Bussgang_GMM.py:186-198) on the device vs the loop restatement."""
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import rate
+    h, he, cov = _data(B=500)
+    g, Cq, _ = rate.bussgang_global(cov, 5.0, n_bits)
+    r = rate.matched_filter_rate(he, h, g, Cq)
+    ro = O.rate_mf(he, h, g, Cq)
+    assert np.isfinite(r) and abs(r - ro) <= 1e-9 * abs(ro)
