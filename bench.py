@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "channel estimates/sec + MSE vs reference; K=128 N=64 full-cov, 1/2/4/8 GPU"
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
+FP64_MFMA_PEAK_TFLOPS = 78.6  # MI355X_MICROARCH.md / SURVEY D3: v_mfma_f64_16x16x4_f64 dense peak (spec)
 FP16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense FP16/BF16 MFMA (spec, no sparsity)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.3 TB/s measured copy)
 
@@ -57,6 +58,8 @@ def parse():
     ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="override B (observations per GPU)")
     ap.add_argument("--shard", default="batch", choices=["batch", "k"])
+    ap.add_argument("--precision", default="f64", choices=["f64", "fast"],
+                    help="dense 'all' arithmetic: f64 (reference complex128, default) or fast (fp16 split)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_metric.json"),
@@ -145,6 +148,8 @@ def main():
 
     if args.shard == "batch":
         model = _lib.DeviceModel(means, covs, w, device=local)
+        if args.precision != "f64":
+            model.set_precision(args.precision)
 
         def step(ev=None):
             model.prepare(None, cfg["snr"], cfg["n_bits"], qkind, thr, lab, stream=sptr)
@@ -238,13 +243,26 @@ def main():
     else:
         flops_per_launch = 16.0 * k_local * N * N * B  # 16 K M N real flops / estimate
         achieved = flops_per_launch / (kern_ms * 1e-3) / 1e12
+        if args.precision == "f64" and not f32_kernel and N <= 64:
+            # FP64 kernel: executed v_mfma_f64_16x16x4 work = 256 flops per sample per 1 KB table block
+            # (GL: NTL(NTL+1) blocks, Linv's upper triangle skipped; GW: NTW * KP blocks)
+            Np = 16 if N <= 16 else (32 if N <= 32 else 64)
+            ntl, ntw, kp = Np // 8, Np // 8, Np // 4
+            executed = 256.0 * (ntl * (ntl + 1) + ntw * kp) * k_local * B
+            roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
+                            frac=round(achieved / FP64_MFMA_PEAK_TFLOPS, 4), traffic=traffic,
+                            kernel="k_est_all_f64 (+k_merge_f64)", peak_dtype="fp64 MFMA (dense)",
+                            kernel_ms=round(kern_ms, 4), flops_per_launch=flops_per_launch,
+                            executed_flops_per_launch=executed,
+                            mfma_issue_frac=round(executed / (kern_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4))
         peak = FP32_MFMA_PEAK_TFLOPS if f32_kernel else FP16_MFMA_PEAK_TFLOPS
         # executed MFMA work: lower-triangular tiles of E(Linv) skipped (R/32 slices of 32x16 tiles) and,
         # for the fp16 kernel, two products (hi, lo) per fp32-class MAC
         nsl = (2 * N) // 32
         tri = (sum(2 * r + 2 for r in range(nsl)) / (nsl * 2 * nsl) + 1.0) / 2.0
         executed = flops_per_launch * tri * (1.0 if f32_kernel else 2.0)
-        roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=peak, unit="TFLOP/s",
+        if not (args.precision == "f64" and not f32_kernel and N <= 64):
+          roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=peak, unit="TFLOP/s",
                         frac=round(achieved / peak, 4), traffic=traffic,
                         kernel=("k_est_all_f32" if f32_kernel else "k_est_all_h2+k_merge_streamk"),
                         peak_dtype="fp32 MFMA" if f32_kernel else "fp16 MFMA (dense)",
@@ -267,8 +285,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak" if args.shard == "batch" else "strong",
             "vs_baseline": None,
-            "dtype": "f64" if fourier else ("f32" if f32_kernel else
-                                            "f16x2 (fp16 hi+lo split, fp32 accumulate, fp64 softmax)"),
+            "dtype": "f64" if (fourier or (args.precision == "f64" and not f32_kernel and N <= 64)) else (
+                "f32" if f32_kernel else "f16x2 (fp16 hi+lo split, fp32 accumulate, fp64 softmax)"),
             "data": f"synthetic: seeded {cfg['cov']} SCM-derived covariances, SCM channel pool + fresh CN noise, "
                     f"{cfg['n_bits']}-bit {cfg['qtype']} quantised",
             "config": {"workload": f"estimate_from_y K={K} N=M={N} cov={cfg['cov']} n_bits={cfg['n_bits']} "

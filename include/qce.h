@@ -51,6 +51,13 @@ typedef struct qce_model qce_model;
                                 (estimators/blmmse.py:53, :86) instead of clip(mean gain, 0, 1)
                                 (gmm_cplx_bussgang.py:304-307); value != 0 enables */
 
+#define QCE_OPT_PRECISION 2 /* arithmetic of the dense 'all' mode and the K-shard partial: QCE_PRECISION_F64 (default,
+                               the reference's complex128 arithmetic: FP64 MFMA products, FP64 accumulation and
+                               softmax) or QCE_PRECISION_FAST (fp16 two-term split products with fp32 accumulation,
+                               ~1e-7 relative; an opt-in throughput mode) */
+#define QCE_PRECISION_F64 0
+#define QCE_PRECISION_FAST 1
+
 #define QCE_IO_HOST 0
 #define QCE_IO_DEVICE 1
 
@@ -94,6 +101,11 @@ int qce_log_prob(qce_model* model, const double* X, int64_t B, double* lp_out, d
  * (B, 2N) f32 interleaved; h = (sum_g acc_g e^{m_g}) / (sum_g s_g e^{m_g}). */
 int qce_estimate_partial(qce_model* model, const double* y, int64_t B, double* m_out, double* s_out, float* acc_out,
                          int io, void* stream);
+
+/* The same partial with an FP64 accumulator acc (B, 2N) f64 interleaved — the format the K-shard combine
+ * all-reduces (one SUM of (s, acc) under a shared shift, sharding.py). */
+int qce_estimate_partial_f64(qce_model* model, const double* y, int64_t B, double* m_out, double* s_out, double* acc_out,
+                             int io, void* stream);
 
 /* Per-SNR tables for state mirroring (the reference mutates gm.means_, gm.covariances_,
  * gm.precisions_cholesky_, :262-313) and tests.  Host pointers, any may be NULL:

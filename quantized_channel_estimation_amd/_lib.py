@@ -14,6 +14,8 @@ LIB_PATH = os.environ.get("QCE_LIB") or os.path.join(_PKG, "libqce.so")  # QCE_L
 QCE_OK, QCE_EARG, QCE_ECHOL, QCE_ENOTIMPL, QCE_EHIP, QCE_ESTATE = range(6)
 MODE_ALL, MODE_TOPN, MODE_CUMP = 0, 1, 2
 OPT_BETA_FIRST = 1
+OPT_PRECISION = 2
+PRECISION_F64, PRECISION_FAST = 0, 1
 QUANT_UNIFORM, QUANT_LLOYD, QUANT_OTHER = 0, 1, 2
 IO_HOST, IO_DEVICE = 0, 1
 
@@ -48,6 +50,7 @@ SIGNATURES = {
     "qce_estimate": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, _vp, ctypes.c_int, _vp]),
     "qce_log_prob": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int, _vp]),
     "qce_estimate_partial": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int, _vp]),
+    "qce_estimate_partial_f64": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int, _vp]),
     "qce_get_tables": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "qce_model_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                       ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
@@ -138,6 +141,7 @@ class DeviceModel:
         self._h = h
         self.K, self.N, self.device = K, N, int(device)
         self.M = 0
+        self.precision = "f64"
 
     @property
     def handle(self):
@@ -244,6 +248,34 @@ class DeviceModel:
         check(load().qce_estimate_partial(self._h, ptr(y), int(B), ptr(m_out), ptr(s_out), ptr(acc_out), io, stream))
         self._order_after(io, stream)
         return m_out, s_out, acc_out
+
+    def partial64(self, y, m_out=None, s_out=None, acc_out=None, stream=None):
+        """K-shard partial with an FP64 accumulator (qce_estimate_partial_f64): (m, s, acc (B, 2N) f64)."""
+        io = IO_HOST if isinstance(y, np.ndarray) else IO_DEVICE
+        B = y.shape[0]
+        if io == IO_HOST:
+            y = np.ascontiguousarray(y, dtype=np.complex128)
+            m_out = np.empty(B) if m_out is None else m_out
+            s_out = np.empty(B) if s_out is None else s_out
+            acc_out = np.empty((B, 2 * self.N)) if acc_out is None else acc_out
+        else:
+            import torch
+            dev = y.device
+            m_out = torch.empty(B, dtype=torch.float64, device=dev) if m_out is None else m_out
+            s_out = torch.empty(B, dtype=torch.float64, device=dev) if s_out is None else s_out
+            acc_out = torch.empty((B, 2 * self.N), dtype=torch.float64, device=dev) if acc_out is None else acc_out
+        self._order_before(y, io, stream)
+        check(load().qce_estimate_partial_f64(self._h, ptr(y), int(B), ptr(m_out), ptr(s_out), ptr(acc_out), io,
+                                              stream))
+        self._order_after(io, stream)
+        return m_out, s_out, acc_out
+
+    def set_precision(self, precision):
+        """'f64' (default: the reference's complex128 arithmetic) or 'fast' (fp16 two-term split products,
+        fp32 accumulation) for the dense 'all' mode and the K-shard partial."""
+        val = {"f64": PRECISION_F64, "fast": PRECISION_FAST}[precision]
+        self.set_option(OPT_PRECISION, val)
+        self.precision = precision
 
     def set_option(self, option, value):
         check(load().qce_model_set_option(self._h, int(option), float(value)))

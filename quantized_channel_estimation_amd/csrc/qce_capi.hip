@@ -66,6 +66,7 @@ struct qce_model {
   int packs_valid = 0;    // pack32 / pack64 built for the current prepare (lazy: 'all' mode never needs them)
   QcePrepareArgs pack_args{};
   int beta_first = 0;  // QCE_OPT_BETA_FIRST: multi-bit Cr mixes with the first gain (blmmse.py:53, :86)
+  int precision = QCE_PRECISION_F64;  // QCE_OPT_PRECISION: arithmetic of the dense 'all' / partial path
   hipStream_t stream = nullptr;
   int has_mean = 0;
   std::vector<double> weights;
@@ -92,6 +93,11 @@ struct qce_model {
   DevBuf<double> sp_m, sp_s;
   DevBuf<float> sp_a;
   DevBuf<int> yflag;
+  // FP64 fused-kernel tables (qce_estimate_f64.hip) and its cut-tile scratch
+  DevBuf<char> pack_f64;
+  int f64_active = 0;  // the last dense prepare packed FP64 tables: 'all' / partial run k_est_all_f64
+  DevBuf<double> fp_m, fp_s, fp_a;
+  DevBuf<double> part_a64;  // FP64 partial accumulator behind the f32 qce_estimate_partial
   int cu_count = 256;
   // Fourier-domain path for (block-)circulant mixtures (qce_fft.hip): structure found at creation
   int fft_n1 = 0, fft_n2 = 0;
@@ -165,6 +171,64 @@ int ensure_packs(qce_model* m, hipStream_t st) {
 bool use_h2() {
   const char* e = getenv("QCE_KERNEL");
   return !(e && strcmp(e, "f32") == 0);
+}
+
+// Arithmetic of the dense 'all' / partial path for this model: the model option, overridden by
+// QCE_KERNEL=f64 | h2 | f32 (A/B runs).
+bool want_f64(const qce_model* m) {
+  const char* e = getenv("QCE_KERNEL");
+  if (e && strcmp(e, "f64") == 0) return true;
+  if (e && (strcmp(e, "h2") == 0 || strcmp(e, "f32") == 0)) return false;
+  return m->precision == QCE_PRECISION_F64;
+}
+
+// 'all' mode in FP64 (qce_estimate_f64.hip): whole tiles data-parallel over one resident workgroup
+// per CU, the remaining tiles' (tile, component) items dealt out stream-K; final h, or the FP64
+// (m, s, acc) partial when h == nullptr (K-shard path)
+int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, double* oa,
+            hipStream_t st) {
+  const long long TS = qce_f64_tile();
+  const long long tiles = (B + TS - 1) / TS;
+  long long slots = m->cu_count;  // 128 KB of LDS: one workgroup per CU
+  const char* e = getenv("QCE_WORKGROUPS");
+  if (e && atoll(e) > 0) slots = atoll(e);
+  long long nwg, R, L;
+  if (tiles >= slots) {
+    nwg = slots;
+    R = tiles / slots;
+    L = ((tiles - R * slots) * m->K + nwg - 1) / nwg;
+  } else {
+    R = 0;
+    L = (tiles * m->K + slots - 1) / slots;
+    if (L < 1) L = 1;
+    nwg = (tiles * m->K + L - 1) / L;
+  }
+  QceF64Args a;
+  a.B = B;
+  a.M = m->M;
+  a.N = m->N;
+  a.K = m->K;
+  a.MP = m->MP;
+  a.NP = m->NP;
+  a.has_mean = m->has_mean;
+  a.nwg = (int)nwg;
+  a.R = (int)R;
+  a.L = L;
+  a.y = dy;
+  a.pack = m->pack_f64.p;
+  a.cconst = m->cconst.p;
+  a.h = h;
+  a.om = om;
+  a.os = os;
+  a.oa = oa;
+  HIPCHK(m->fp_m.ensure((size_t)nwg * 2 * TS));
+  HIPCHK(m->fp_s.ensure((size_t)nwg * 2 * TS));
+  HIPCHK(m->fp_a.ensure((size_t)nwg * 2 * TS * 2 * m->N));
+  a.pm = m->fp_m.p;
+  a.ps = m->fp_s.p;
+  a.pa = m->fp_a.p;
+  HIPCHK(qce_launch_est_f64(a, h == nullptr, st));
+  return QCE_OK;
 }
 
 int run_h2x(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, float* oa,
@@ -475,6 +539,8 @@ int qce_model_destroy(qce_model* m) {
   m->sp_s.release();
   m->sp_a.release();
   m->yflag.release();
+  m->pack_f64.release();
+  for (auto* b : {&m->fp_m, &m->fp_s, &m->fp_a, &m->part_a64}) b->release();
   for (auto* b : {&m->f_ceig, &m->f_rinvT, &m->f_cprime, &m->f_wT, &m->f_gain}) b->release();
   for (auto* b : {&m->f_col0, &m->f_mspec, &m->f_uT, &m->f_bT}) b->release();
   m->f_bad.release();
@@ -742,19 +808,27 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
   p.pack32 = nullptr;  // selective-mode / log-prob tables are packed on first use (ensure_packs)
   p.pack64 = nullptr;
   HIPCHK(qce_launch_prepare(p, st));
-  // FP16 two-term split tables; the observation scale makes quantiser outputs exact in fp16
-  // (1 bit: y sqrt(2) = +-1; uniform: y 2/delta = odd integers), folded into the slice scales
-  double y_scale = 1.0;
-  if (kind == 0) y_scale = sqrt(2.0);
-  else if (kind == 1 && quant_kind == QCE_QUANT_UNIFORM && delta > 0.0) y_scale = 2.0 / delta;
-  const long long cs16 = qce_pack_h2_stride_bytes(MP, NP, m->has_mean);
-  const int nslices = (2 * MP) / 32 + (2 * NP) / 32;
-  HIPCHK(m->pack16.ensure((size_t)cs16 * K + (size_t)qce_h2x_pad_bytes()));
-  HIPCHK(m->sinv.ensure((size_t)nslices * K));
-  HIPCHK(qce_launch_pack_h2(K, M, N, MP, NP, m->has_mean, cs16, y_scale, m->Linv.p, m->W.p, m->q0.p, m->bvec.p,
-                            m->pack16.p, m->sinv.p, st));
-  m->cstride16 = cs16;
-  m->y_scale = y_scale;
+  m->f64_active = want_f64(m) && qce_f64_shape(MP, NP);
+  if (m->f64_active) {
+    // FP64 tables of the fused kernel (reference precision)
+    HIPCHK(m->pack_f64.ensure((size_t)qce_pack_f64all_bytes(MP, NP, m->has_mean) * K));
+    HIPCHK(qce_launch_pack_f64all(K, M, N, MP, NP, m->has_mean, m->Linv.p, m->W.p, m->q0.p, m->bvec.p,
+                                  reinterpret_cast<double*>(m->pack_f64.p), st));
+  } else {
+    // FP16 two-term split tables; the observation scale makes quantiser outputs exact in fp16
+    // (1 bit: y sqrt(2) = +-1; uniform: y 2/delta = odd integers), folded into the slice scales
+    double y_scale = 1.0;
+    if (kind == 0) y_scale = sqrt(2.0);
+    else if (kind == 1 && quant_kind == QCE_QUANT_UNIFORM && delta > 0.0) y_scale = 2.0 / delta;
+    const long long cs16 = qce_pack_h2_stride_bytes(MP, NP, m->has_mean);
+    const int nslices = (2 * MP) / 32 + (2 * NP) / 32;
+    HIPCHK(m->pack16.ensure((size_t)cs16 * K + (size_t)qce_h2x_pad_bytes()));
+    HIPCHK(m->sinv.ensure((size_t)nslices * K));
+    HIPCHK(qce_launch_pack_h2(K, M, N, MP, NP, m->has_mean, cs16, y_scale, m->Linv.p, m->W.p, m->q0.p, m->bvec.p,
+                              m->pack16.p, m->sinv.p, st));
+    m->cstride16 = cs16;
+    m->y_scale = y_scale;
+  }
   std::vector<int> status(K);
   HIPCHK(hipMemcpyAsync(status.data(), m->status.p, sizeof(int) * K, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
@@ -823,7 +897,9 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
       HIPCHK(qce_launch_fft_est(fa, 2, st));
     }
   } else if (mode == QCE_MODE_ALL) {
-    if (use_h2() || !qce_shape_supported(m->MP, m->NP)) {
+    if (m->f64_active) {
+      if ((rc = run_f64(m, dy, B, dh, nullptr, nullptr, nullptr, st))) return rc;
+    } else if (use_h2() || !qce_shape_supported(m->MP, m->NP)) {
       if ((rc = run_h2(m, dy, B, dh, nullptr, nullptr, nullptr, st))) return rc;
     } else {
       HIPCHK(qce_launch_est_all(a, dh, st));
@@ -927,6 +1003,10 @@ int qce_estimate_partial(qce_model* m, const double* y, int64_t B, double* m_out
     fa.oa = da;
     if (m->fft_mfma) HIPCHK(qce_launch_fft_mfma(fa, 3, st));
     else HIPCHK(qce_launch_fft_est(fa, 3, st));
+  } else if (m->f64_active) {  // FP64 partial, rounded to the f32 accumulator of this entry point
+    HIPCHK(m->part_a64.ensure((size_t)B * 2 * m->N));
+    if ((rc = run_f64(m, dy, B, nullptr, dm, ds, m->part_a64.p, st))) return rc;
+    HIPCHK(qce_launch_f64_to_f32(m->part_a64.p, da, (long long)B * 2 * m->N, st));
   } else if (use_h2() || !qce_shape_supported(m->MP, m->NP)) {
     if ((rc = run_h2(m, dy, B, nullptr, dm, ds, da, st))) return rc;
   } else {
@@ -938,6 +1018,43 @@ int qce_estimate_partial(qce_model* m, const double* y, int64_t B, double* m_out
     HIPCHK(hipMemcpyAsync(m_out, dm, sizeof(double) * B, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(s_out, ds, sizeof(double) * B, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(acc_out, da, sizeof(float) * (size_t)B * 2 * m->N, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return QCE_OK;
+}
+
+int qce_estimate_partial_f64(qce_model* m, const double* y, int64_t B, double* m_out, double* s_out, double* acc_out,
+                             int io, void* stream) {
+  int rc = check_model(m, true);
+  if (rc) return rc;
+  if (B < 0 || (B > 0 && (!y || !m_out || !s_out || !acc_out))) return fail(QCE_EARG, "bad arguments");
+  if (B == 0) return QCE_OK;
+  DeviceGuard g(m->device);
+  hipStream_t st = pick_stream(m, stream);
+  const double2* dy = nullptr;
+  if ((rc = stage_input(m, y, B, io, st, &dy))) return rc;
+  double *dm = m_out, *ds = s_out, *da = acc_out;
+  if (io == QCE_IO_HOST) {
+    HIPCHK(m->m_scr.ensure((size_t)B));
+    HIPCHK(m->s_scr.ensure((size_t)B));
+    HIPCHK(m->part_a64.ensure((size_t)B * 2 * m->N));
+    dm = m->m_scr.p;
+    ds = m->s_scr.p;
+    da = m->part_a64.p;
+  }
+  if (!m->fft_active && m->f64_active) {
+    if ((rc = run_f64(m, dy, B, nullptr, dm, ds, da, st))) return rc;
+  } else {  // Fourier / fast paths keep an f32 accumulator: widen it
+    HIPCHK(m->acc_scr.ensure((size_t)B * 2 * m->N));
+    if ((rc = qce_estimate_partial(m, reinterpret_cast<const double*>(dy), B, dm, ds, m->acc_scr.p, QCE_IO_DEVICE,
+                                   st)))
+      return rc;
+    HIPCHK(qce_launch_f32_to_f64(m->acc_scr.p, da, (long long)B * 2 * m->N, st));
+  }
+  if (io == QCE_IO_HOST) {
+    HIPCHK(hipMemcpyAsync(m_out, dm, sizeof(double) * B, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(s_out, ds, sizeof(double) * B, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(acc_out, da, sizeof(double) * (size_t)B * 2 * m->N, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
   }
   return QCE_OK;
@@ -1220,6 +1337,12 @@ int qce_model_set_option(qce_model* m, int option, double value) {
   if (!m) return fail(QCE_EARG, "null model");
   if (option == QCE_OPT_BETA_FIRST) {
     m->beta_first = value != 0.0;
+    m->prepared = 0;
+    return QCE_OK;
+  }
+  if (option == QCE_OPT_PRECISION) {
+    if (value != QCE_PRECISION_F64 && value != QCE_PRECISION_FAST) return fail(QCE_EARG, "unknown precision");
+    m->precision = (int)value;
     m->prepared = 0;
     return QCE_OK;
   }

@@ -1,0 +1,542 @@
+// Fused 'all'-mode estimate kernel in FP64 on v_mfma_f64_16x16x4_f64 (gfx950 / CDNA4) — the
+// reference-precision path of estimate_from_y (gmm_cplx_bussgang.py:220-228 with :331-332,
+// :388-435, :632-656; every reference step is complex128).
+//
+//   lp_bk = c_k - || E(Linv_k) [y_b; 1] ||^2          (the -q0 column folds the mean in)
+//   h_b   = sum_k e^{lp_bk - m_b} E(W_k) [y_b; 1] / sum_k e^{lp_bk - m_b}
+//
+// E(.) is the real 2x2-block embedding of a complex matrix; every product is an FP64 MFMA with
+// FP64 accumulation, the softmax is FP64 (libm exp), so the result is an FP64 computation of the
+// reference's formula (only the summation order differs).
+//
+// Layout (prepare: k_pack_f64all).  The k (reduction) order is permuted so that one 16-byte load
+// of y gives a lane both B-operand values of a "k-pair": k-step 2s+e, lane group g = lane>>4
+// holds part e of complex column 4s+g.  Output rows are permuted so that a lane's four
+// accumulator registers are (re, im) of complex rows 8T+g and 8T+4+g: row rho of row tile T is
+// complex 8T + 4(rho>>3) + (rho&3), part (rho>>2)&1.  A table "block" is 1 KB: the A operands of
+// one row tile for the two k-steps of a k-pair, lane-major (lane l: 16 B = both k-steps), read
+// with one conflict-free ds_read_b128.
+//   component k: GL blocks (row tile T outer; k-pairs 0..2T+1 — the upper triangle of Linv is
+//   skipped; + one mean block with the -q0 column), then GW blocks (k-pair outer, row tile inner,
+//   + one mean block per row tile with the b column), padded to whole ring chunks.
+//
+// Scheduling: one workgroup = NW waves x 16*CT samples (CT column tiles per wave; samples on the
+// MFMA column axis, so quad form, running max, sum and weights are per-lane registers and the
+// y fragments stay in VGPRs for the whole component loop).  The component tables stream through
+// an LDS ring of NSLOT chunks of 16 KB (global_load_lds, 16 B per lane); one barrier per chunk,
+// executed E blocks before the chunk is needed so the LDS reads of its first blocks are not held
+// up.  Persistent grid: R rounds of whole tiles per workgroup, then the remaining tiles' (tile,
+// component) items dealt out L per workgroup (stream-K); a tile cut between workgroups leaves
+// FP64 partials (m, s, acc) that k_merge_f64 combines — the same format as the K-shard path.
+#include "qce_common.h"
+#include "qce_kernels.h"
+#include "qce_h2_common.h"
+
+#include <utility>
+
+namespace {
+
+template <int MP, int NP, bool HM>
+struct F64G {
+  static constexpr int NTL = MP / 8;  // GL row tiles (16 real rows = 8 complex rows)
+  static constexpr int NTW = NP / 8;  // GW row tiles
+  static constexpr int KP = MP / 4;   // k-pairs (4 complex columns)
+  static constexpr int HMI = HM ? 1 : 0;
+  static constexpr int GL_BLOCKS = NTL * (NTL + 1) + HMI * NTL;
+  static constexpr int GW_BLOCKS = NTW * (KP + HMI);
+  static constexpr int BLOCKS = GL_BLOCKS + GW_BLOCKS;
+  static constexpr int CB = 16;  // blocks per ring chunk (16 KB)
+  static constexpr int BPC = (BLOCKS + CB - 1) / CB * CB;
+  static constexpr int CPC = BPC / CB;
+  static constexpr __host__ __device__ int gl_off(int T) { return T * (T + 1) + HMI * T; }
+};
+
+constexpr int F64_NSLOT = 8;                // ring slots (128 KB of LDS)
+constexpr int F64_CHUNK = 16 * 1024;
+
+// block b of a component -> kind (0 GL data, 1 GL mean, 2 GW data, 3 GW mean, 4 pad), tile T, k-pair s
+struct BlockInfo {
+  int kind, T, s;
+};
+template <int MP, int NP, bool HM>
+constexpr BlockInfo block_info(int b) {
+  using G = F64G<MP, NP, HM>;
+  if (b < G::GL_BLOCKS) {
+    int T = 0;
+    while (b >= G::gl_off(T + 1)) ++T;
+    const int s = b - G::gl_off(T);
+    return BlockInfo{s < 2 * T + 2 ? 0 : 1, T, s};
+  }
+  const int r = b - G::GL_BLOCKS;
+  if (r < G::KP * G::NTW) return BlockInfo{2, r % G::NTW, r / G::NTW};
+  if (r < (G::KP + G::HMI) * G::NTW) return BlockInfo{3, r - G::KP * G::NTW, G::KP};
+  return BlockInfo{4, 0, 0};
+}
+
+template <int N_>
+QCE_DEV void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N_) : "memory");
+}
+
+QCE_DEV double sum_groups(double q) {  // sum over the four 16-lane groups (all lanes get the total)
+  q += __shfl_xor(q, 16);
+  q += __shfl_xor(q, 32);
+  return q;
+}
+
+// Source cursor of the ring: which component chunk a workgroup streams next.  Items are the
+// workgroup's (tile, component) work in order: R*K full-round items (components 0..K-1 per tile),
+// then the tail items item0 .. item0+ntail-1 (component = item % K).
+struct RingCursor {
+  int item, nitems, rk, comp_tail, comp, cc, K, cpc;
+  QCE_DEV void init(int rk_, int comp_tail_, int ntail, int K_, int cpc_) {
+    rk = rk_;
+    comp_tail = comp_tail_;
+    nitems = rk_ + ntail;
+    K = K_;
+    cpc = cpc_;
+    item = 0;
+    cc = 0;
+    comp = rk_ > 0 ? 0 : comp_tail_;
+  }
+  QCE_DEV long long chunk_index() const { return (long long)(comp * cpc + cc); }
+  QCE_DEV void advance() {
+    if (item >= nitems) return;
+    if (++cc < cpc) return;
+    cc = 0;
+    ++item;
+    if (item >= nitems) {  // past the end: keep re-loading the last chunk (dummy, never read)
+      item = nitems;
+      cc = cpc - 1;
+      return;
+    }
+    if (item == rk) comp = comp_tail;
+    else comp = (comp + 1 == K) ? 0 : comp + 1;
+  }
+};
+
+// one chunk = 16 wave-instructions of 1 KB, LPW per wave (wave-uniform addresses, no branches)
+template <int NW>
+QCE_DEV void issue_chunk(const char* __restrict__ src, char* dst, int wave, int lane) {
+  constexpr int LPW = (F64_CHUNK / 1024) / NW;
+  src += wave * 1024 + lane * 16;
+  dst += wave * 1024;
+#pragma unroll
+  for (int i = 0; i < LPW; ++i)
+    __builtin_amdgcn_global_load_lds((const void*)(src + i * NW * 1024),
+                                     (__attribute__((address_space(3))) void*)(dst + i * NW * 1024), 16, 0, 0);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// fused kernel
+// ---------------------------------------------------------------------------
+template <int MP, int NP, bool HM, int CT, int NW, bool OUT_PARTIAL>
+__global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int N, int K, int R, long long L,
+                                                         const double2* __restrict__ y, const char* __restrict__ pack,
+                                                         const double* __restrict__ cconst, double2* __restrict__ h,
+                                                         double* __restrict__ om, double* __restrict__ os,
+                                                         double* __restrict__ oa, double* __restrict__ pm,
+                                                         double* __restrict__ ps, double* __restrict__ pa) {
+  using G = F64G<MP, NP, HM>;
+  constexpr int TS = NW * 16 * CT;           // samples per tile
+  constexpr int LPW = (F64_CHUNK / 1024) / NW;  // global_load_lds per wave per chunk
+  constexpr int E = 2;                        // boundary lead (blocks) = LDS prefetch distance
+  constexpr double RESCALE = 32.0;            // lazy max: rescale only when lp exceeds m by this
+  static_assert((F64_CHUNK / 1024) % NW == 0, "chunk split");
+  __shared__ __attribute__((aligned(16))) char lds[F64_NSLOT * F64_CHUNK];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, col = lane & 15;
+  const long long P = gridDim.x, w = blockIdx.x;
+  const long long tiles = (B + TS - 1) / TS;
+  const long long tail0 = (long long)R * P;
+  const long long item0 = w * L;
+  const long long tail_items = (tiles - tail0) * K;
+  const long long item1 = (item0 + L < tail_items) ? item0 + L : tail_items;
+  const long long ntail = item1 > item0 ? item1 - item0 : 0;
+  if ((long long)R == 0 && ntail == 0) return;  // nothing for this workgroup (uniform)
+  const long long t_first = tail0 + (L > 0 ? item0 / K : 0);
+  const long long nseg = (long long)R + (ntail > 0 ? (item1 - 1) / K - item0 / K + 1 : 0);
+
+  // ---- ring ----
+  RingCursor cur;
+  cur.init(R * K, (int)(item0 % K), (int)ntail, K, G::CPC);
+  int issued = 0;  // chunks issued so far (stream index of the next one)
+  auto issue_next = [&]() {
+    const char* src = pack + cur.chunk_index() * (long long)F64_CHUNK;
+    char* dst = lds + (issued & (F64_NSLOT - 1)) * F64_CHUNK;
+    issue_chunk<NW>(src, dst, wave, lane);
+    cur.advance();
+    ++issued;
+  };
+  // boundary for stream chunk jn: its loads landed everywhere, and every wave is done with chunk
+  // jn - 2, whose slot is refilled with chunk jn + NSLOT - 2
+  auto boundary = [&]() {
+    wait_vmcnt<(F64_NSLOT - 3) * LPW>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    issue_next();
+  };
+#pragma unroll 1
+  for (int j = 0; j < F64_NSLOT - 2; ++j) issue_next();
+  boundary();  // chunk 0
+  int cstream = 0;  // stream index of the current component's chunk 0
+
+  for (long long seg = 0; seg < nseg; ++seg) {
+    long long t;
+    int klo, khi;
+    if (seg < R) {
+      t = seg * P + w;
+      klo = 0;
+      khi = K;
+    } else {
+      t = tail0 + item0 / K + (seg - R);
+      const long long tK = (t - tail0) * K;
+      klo = (int)((item0 > tK ? item0 : tK) - tK);
+      khi = (int)((tK + K < item1 ? tK + K : item1) - tK);
+    }
+    const long long sbase = t * TS + (long long)wave * 16 * CT;
+    // y fragments: k-pair s, lane group g -> complex column 4s + g (re: k-step 2s, im: 2s+1)
+    double2 yv[CT][G::KP];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const long long sm = sbase + 16 * c + col;
+#pragma unroll
+      for (int s = 0; s < G::KP; ++s) {
+        const int cc = 4 * s + g;
+        yv[c][s] = (sm < B && cc < M) ? y[sm * M + cc] : make_double2(0.0, 0.0);
+      }
+    }
+    wait_vmcnt<0>();
+    f64x4 out[G::NTW][CT];
+#pragma unroll
+    for (int T = 0; T < G::NTW; ++T)
+#pragma unroll
+      for (int c = 0; c < CT; ++c) out[T][c] = f64x4{0.0, 0.0, 0.0, 0.0};
+    double m[CT], ssum[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      m[c] = QCE_NEG_INF;
+      ssum[c] = 0.0;
+    }
+
+#pragma unroll 1
+    for (int k = klo; k < khi; ++k) {
+      const double ck = cconst[k];
+      const int slot0 = cstream & (F64_NSLOT - 1);
+      const char* lane_base = lds + lane * 16;
+      auto blk = [&](int b) -> const double2* {
+        const int slot = (slot0 + b / G::CB) & (F64_NSLOT - 1);
+        return reinterpret_cast<const double2*>(lane_base + slot * F64_CHUNK + (b % G::CB) * 1024);
+      };
+      f64x4 acc[CT];
+      double qp[CT], p[CT];
+      double bs0[CT], bs1[CT];
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        qp[c] = 0.0;
+        p[c] = 0.0;
+        bs0[c] = bs1[c] = 0.0;
+        acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
+      }
+      double2 buf[E + 1];
+#pragma unroll
+      for (int i = 0; i < E; ++i) buf[i] = *blk(i);
+      static_for(
+          [&](auto bc) {
+            constexpr int b = decltype(bc)::value;
+            constexpr BlockInfo bi = block_info<MP, NP, HM>(b);
+            __builtin_amdgcn_sched_barrier(0);  // keep the explicit prefetch distance (no LDS read hoisting)
+            // next chunk's boundary E blocks early (the last one is the next component's chunk 0)
+            if constexpr ((b + E) % G::CB == 0) boundary();
+            if constexpr (b + E < G::BPC) buf[(b + E) % (E + 1)] = *blk(b + E);
+            const double2 a = buf[b % (E + 1)];
+            if constexpr (bi.kind == 0) {  // GL data: u += E(Linv) y over k-pair s
+#pragma unroll
+              for (int c = 0; c < CT; ++c) acc[c] = mfma16x16x4d(a.x, yv[c][bi.s].x, acc[c]);
+#pragma unroll
+              for (int c = 0; c < CT; ++c) acc[c] = mfma16x16x4d(a.y, yv[c][bi.s].y, acc[c]);
+            } else if constexpr (bi.kind == 1) {  // GL mean column (-q0): B = 1 in lane group 0
+              const double one = g == 0 ? 1.0 : 0.0;
+#pragma unroll
+              for (int c = 0; c < CT; ++c) acc[c] = mfma16x16x4d(a.x, one, acc[c]);
+            } else if constexpr (bi.kind == 2) {  // GW data: out += E(W) (p y) over k-pair s
+              if constexpr (bi.T == 0) {
+#pragma unroll
+                for (int c = 0; c < CT; ++c) {
+                  bs0[c] = yv[c][bi.s].x * p[c];
+                  bs1[c] = yv[c][bi.s].y * p[c];
+                }
+              }
+#pragma unroll
+              for (int c = 0; c < CT; ++c) out[bi.T][c] = mfma16x16x4d(a.x, bs0[c], out[bi.T][c]);
+#pragma unroll
+              for (int c = 0; c < CT; ++c) out[bi.T][c] = mfma16x16x4d(a.y, bs1[c], out[bi.T][c]);
+            } else if constexpr (bi.kind == 3) {  // GW mean column (b): B = p in lane group 0
+#pragma unroll
+              for (int c = 0; c < CT; ++c) out[bi.T][c] = mfma16x16x4d(a.x, g == 0 ? p[c] : 0.0, out[bi.T][c]);
+            }
+            // end of a GL row tile: fold its squares into the quad form
+            if constexpr (bi.kind == 0 || bi.kind == 1) {
+              constexpr bool last = HM ? (bi.kind == 1) : (bi.s == 2 * bi.T + 1);
+              if constexpr (last) {
+#pragma unroll
+                for (int c = 0; c < CT; ++c) {
+                  qp[c] = fma(acc[c][0], acc[c][0], qp[c]);
+                  qp[c] = fma(acc[c][1], acc[c][1], qp[c]);
+                  qp[c] = fma(acc[c][2], acc[c][2], qp[c]);
+                  qp[c] = fma(acc[c][3], acc[c][3], qp[c]);
+                  // pin the fold here: sunk to the softmax, every row tile would keep its own accumulators
+                  asm volatile("" : "+v"(qp[c]));
+                  acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
+                }
+              }
+            }
+            // after the last GL block: log-probability and the online softmax (FP64)
+            if constexpr (b == G::GL_BLOCKS - 1) {
+              double lp[CT];
+              bool need = false;
+#pragma unroll
+              for (int c = 0; c < CT; ++c) {
+                lp[c] = ck - sum_groups(qp[c]);
+                need = need || (lp[c] > m[c] + RESCALE);
+              }
+              if (__builtin_amdgcn_ballot_w64(need) != 0ull) {  // rare: new running maximum
+#pragma unroll
+                for (int c = 0; c < CT; ++c) {
+                  const bool up = lp[c] > m[c] + RESCALE;
+                  const double mn = up ? lp[c] : m[c];
+                  const double al = up ? (m[c] == QCE_NEG_INF ? 0.0 : exp(m[c] - mn)) : 1.0;
+                  ssum[c] *= al;
+                  m[c] = mn;
+#pragma unroll
+                  for (int T = 0; T < G::NTW; ++T) out[T][c] *= al;
+                }
+              }
+#pragma unroll
+              for (int c = 0; c < CT; ++c) {
+                p[c] = (lp[c] == QCE_NEG_INF) ? 0.0 : exp(lp[c] - m[c]);
+                ssum[c] += p[c];
+              }
+            }
+          },
+          std::make_integer_sequence<int, G::BPC>{});
+      cstream += G::CPC;
+    }
+
+    // ---- write the tile ----
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const int ls = wave * 16 * CT + 16 * c + col;
+      const long long sample = t * TS + ls;
+      if (sample >= B) continue;
+      const bool whole = (klo == 0 && khi == K);
+      const bool pfmt = OUT_PARTIAL || !whole;
+      const long long row = whole ? sample : (w * 2 + (t == t_first ? 0 : 1)) * TS + ls;
+      if (pfmt) {
+        double* dm = whole ? om : pm;
+        double* ds = whole ? os : ps;
+        double* da = (whole ? oa : pa) + row * (2LL * N);
+        if (g == 0) {
+          dm[row] = m[c];
+          ds[row] = ssum[c];
+        }
+#pragma unroll
+        for (int T = 0; T < G::NTW; ++T) {
+          const int i0 = 8 * T + g, i1 = 8 * T + 4 + g;
+          if (i0 < N) *reinterpret_cast<double2*>(da + 2 * i0) = make_double2(out[T][c][0], out[T][c][1]);
+          if (i1 < N) *reinterpret_cast<double2*>(da + 2 * i1) = make_double2(out[T][c][2], out[T][c][3]);
+        }
+      } else {
+        const double inv = 1.0 / ssum[c];
+        double2* hp = h + sample * N;
+#pragma unroll
+        for (int T = 0; T < G::NTW; ++T) {
+          const int i0 = 8 * T + g, i1 = 8 * T + 4 + g;
+          if (i0 < N) hp[i0] = make_double2(out[T][c][0] * inv, out[T][c][1] * inv);
+          if (i1 < N) hp[i1] = make_double2(out[T][c][2] * inv, out[T][c][3] * inv);
+        }
+      }
+    }
+  }
+  wait_vmcnt<0>();  // drain the (dummy) ring prefetches before the workgroup retires
+}
+
+// Combine the stream-K pieces of tiles cut between workgroups (one wave per sample; tiles written
+// whole return at once): h = sum_j acc_j e^{m_j - M} / sum_j s_j e^{m_j - M}, or the merged partial.
+__global__ __launch_bounds__(256) void k_merge_f64(long long B, int N, int K, int TS, long long L,
+                                                   const double* __restrict__ pm, const double* __restrict__ ps,
+                                                   const double* __restrict__ pa, double2* __restrict__ h,
+                                                   double* __restrict__ om, double* __restrict__ os,
+                                                   double* __restrict__ oa) {
+  const long long b = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= B || L <= 0) return;
+  const long long t = b / TS, ls = b % TS;
+  const long long wa = (t * K) / L, wb = ((t + 1) * K - 1) / L;
+  if (wa == wb) return;
+  auto rec_of = [&](long long w) -> long long {
+    const long long tf = (w * L) / K;
+    return (w * 2 + (t == tf ? 0 : 1)) * TS + ls;
+  };
+  double mx = QCE_NEG_INF;
+  for (long long w = wa; w <= wb; ++w) mx = fmax(mx, pm[rec_of(w)]);
+  double s = 0.0;
+  for (long long w = wa; w <= wb; ++w) {
+    const long long r = rec_of(w);
+    s += (pm[r] == QCE_NEG_INF) ? 0.0 : ps[r] * exp(pm[r] - mx);
+  }
+  for (int n = lane; n < N; n += 64) {
+    double re = 0.0, im = 0.0;
+    for (long long w = wa; w <= wb; ++w) {
+      const long long r = rec_of(w);
+      const double sc = (pm[r] == QCE_NEG_INF) ? 0.0 : exp(pm[r] - mx);
+      const double2 v = *reinterpret_cast<const double2*>(pa + r * 2 * N + 2 * n);
+      re = fma(v.x, sc, re);
+      im = fma(v.y, sc, im);
+    }
+    if (h) {
+      h[b * N + n] = make_double2(re / s, im / s);
+    } else {
+      *reinterpret_cast<double2*>(oa + b * 2 * N + 2 * n) = make_double2(re, im);
+    }
+  }
+  if (!h && lane == 0) {
+    om[b] = mx;
+    os[b] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// prepare-side packing of the FP64 tables (one 64-thread group per 1 KB block)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_pack_f64all(int M, int N, int MP, int NP, int has_mean, int bpc,
+                                                    const double2* __restrict__ Linv, const double2* __restrict__ W,
+                                                    const double2* __restrict__ q0, const double2* __restrict__ bvec,
+                                                    double* __restrict__ pack) {
+  const int b = blockIdx.x, k = blockIdx.y, lane = threadIdx.x;
+  const int NTL = MP / 8, NTW = NP / 8, KP = MP / 4, HMI = has_mean ? 1 : 0;
+  const int gl_blocks = NTL * (NTL + 1) + HMI * NTL;
+  int kind = 4, T = 0, s = 0;
+  if (b < gl_blocks) {
+    while (b >= (T + 1) * (T + 2) + HMI * (T + 1)) ++T;
+    s = b - (T * (T + 1) + HMI * T);
+    kind = s < 2 * T + 2 ? 0 : 1;
+  } else {
+    const int r = b - gl_blocks;
+    if (r < KP * NTW) {
+      kind = 2;
+      s = r / NTW;
+      T = r % NTW;
+    } else if (r < (KP + HMI) * NTW) {
+      kind = 3;
+      T = r - KP * NTW;
+    }
+  }
+  const int rho = lane & 15, gk = lane >> 4;
+  const int i = 8 * T + 4 * (rho >> 3) + (rho & 3), a = (rho >> 2) & 1;
+  const bool isL = kind <= 1;
+  const int rows = isL ? M : N;
+  double v[2] = {0.0, 0.0};
+  if (kind == 0 || kind == 2) {
+    const int j = 4 * s + gk;
+    if (i < rows && j < M) {
+      const double2 z = isL ? Linv[((long long)k * M + i) * M + j] : W[((long long)k * N + i) * M + j];
+      v[0] = a == 0 ? z.x : z.y;   // k-step 2s: real part of column j
+      v[1] = a == 0 ? -z.y : z.x;  // k-step 2s+1: imaginary part of column j
+    }
+  } else if ((kind == 1 || kind == 3) && gk == 0 && i < rows) {
+    const double2 z = isL ? q0[(long long)k * M + i] : bvec[(long long)k * N + i];
+    const double o = a == 0 ? z.x : z.y;
+    v[0] = isL ? -o : o;
+  }
+  *reinterpret_cast<double2*>(pack + (((long long)k * bpc + b) * 64 + lane) * 2) = make_double2(v[0], v[1]);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int F64_CT = 2, F64_NW = 4;
+constexpr int F64_TS = F64_NW * 16 * F64_CT;
+
+int blocks_per_comp(int MP, int NP, int hm) {
+  const int NTL = MP / 8, NTW = NP / 8, KP = MP / 4, HMI = hm ? 1 : 0;
+  const int n = NTL * (NTL + 1) + HMI * NTL + NTW * (KP + HMI);
+  return (n + 15) / 16 * 16;
+}
+}  // namespace
+
+bool qce_f64_shape(int MP, int NP) {
+  auto ok = [](int v) { return v == 16 || v == 32 || v == 64; };
+  return ok(MP) && ok(NP);
+}
+int qce_f64_tile() { return F64_TS; }
+long long qce_pack_f64all_bytes(int MP, int NP, int has_mean) { return (long long)blocks_per_comp(MP, NP, has_mean) * 1024; }
+
+hipError_t qce_launch_pack_f64all(int K, int M, int N, int MP, int NP, int has_mean, const double2* Linv,
+                                  const double2* W, const double2* q0, const double2* bvec, double* pack,
+                                  hipStream_t st) {
+  const int bpc = blocks_per_comp(MP, NP, has_mean);
+  hipLaunchKernelGGL(k_pack_f64all, dim3(bpc, K), dim3(64), 0, st, M, N, MP, NP, has_mean, bpc, Linv, W, q0, bvec,
+                     pack);
+  return hipGetLastError();
+}
+
+template <int MP, int NP, bool HM, bool OP>
+static hipError_t launch_f64_t(const QceF64Args& a, hipStream_t st) {
+  hipLaunchKernelGGL((k_est_all_f64<MP, NP, HM, F64_CT, F64_NW, OP>), dim3((unsigned)a.nwg), dim3(F64_NW * 64), 0, st,
+                     a.B, a.M, a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa);
+  return hipGetLastError();
+}
+
+#define QCE_F64_SHAPES(X) \
+  X(16, 16) X(16, 32) X(16, 64) X(32, 16) X(32, 32) X(32, 64) X(64, 16) X(64, 32) X(64, 64)
+
+hipError_t qce_launch_est_f64(const QceF64Args& a, bool out_partial, hipStream_t st) {
+  hipError_t e = hipErrorInvalidValue;
+  const bool hm = a.has_mean != 0;
+#define QCE_CASE(X, Y)                                                                                            \
+  if (a.MP == X && a.NP == Y) {                                                                                   \
+    if (out_partial) e = hm ? launch_f64_t<X, Y, true, true>(a, st) : launch_f64_t<X, Y, false, true>(a, st);     \
+    else e = hm ? launch_f64_t<X, Y, true, false>(a, st) : launch_f64_t<X, Y, false, false>(a, st);               \
+  }
+  QCE_F64_SHAPES(QCE_CASE)
+#undef QCE_CASE
+  if (e != hipSuccess) return e;
+  const long long tiles = (a.B + F64_TS - 1) / F64_TS;
+  const long long tail0 = (long long)a.R * a.nwg;
+  if (a.L > 0 && tiles > tail0) {  // some tail tile may be cut between workgroups
+    const long long b0 = tail0 * F64_TS;
+    const long long nb = a.B - b0;
+    hipLaunchKernelGGL(k_merge_f64, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, st, nb, a.N, a.K, F64_TS, a.L,
+                       a.pm, a.ps, a.pa, out_partial ? nullptr : a.h + b0 * a.N, a.om ? a.om + b0 : nullptr,
+                       a.os ? a.os + b0 : nullptr, a.oa ? a.oa + b0 * 2 * a.N : nullptr);
+    e = hipGetLastError();
+  }
+  return e;
+}
+
+// precision conversions between the f32 and FP64 partial accumulators
+__global__ __launch_bounds__(256) void k_f64_to_f32(const double* __restrict__ a, float* __restrict__ b, long long n) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) b[i] = (float)a[i];
+}
+__global__ __launch_bounds__(256) void k_f32_to_f64(const float* __restrict__ a, double* __restrict__ b, long long n) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) b[i] = (double)a[i];
+}
+hipError_t qce_launch_f64_to_f32(const double* a, float* b, long long n, hipStream_t st) {
+  long long blocks = (n + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks);
+  hipLaunchKernelGGL(k_f64_to_f32, dim3((unsigned)blocks), dim3(256), 0, st, a, b, n);
+  return hipGetLastError();
+}
+hipError_t qce_launch_f32_to_f64(const float* a, double* b, long long n, hipStream_t st) {
+  long long blocks = (n + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks);
+  hipLaunchKernelGGL(k_f32_to_f64, dim3((unsigned)blocks), dim3(256), 0, st, a, b, n);
+  return hipGetLastError();
+}

@@ -81,6 +81,30 @@ hipError_t qce_launch_pack_h2(int K, int M, int N, int MP, int NP, int has_mean,
 hipError_t qce_launch_est_h2(const QceH2Args& a, bool out_partial, hipStream_t st);
 int qce_h2_blocks_per_cu(int MP, int NP, int has_mean);
 
+// FP64 fused 'all' kernel (qce_estimate_f64.hip): the reference-precision path, stream-K scheduled
+struct QceF64Args {
+  long long B;
+  int M, N, K, MP, NP, has_mean;
+  int nwg;      // persistent workgroups P
+  int R;        // data-parallel rounds of whole tiles
+  long long L;  // stream-K tail: (tile, component) items per workgroup
+  const double2* y;
+  const char* pack;  // K x qce_pack_f64all_bytes
+  const double* cconst;
+  double2* h;           // final output (or nullptr with out_partial)
+  double *om, *os, *oa;  // partial-format output (K-shard path), oa B x 2N
+  double *pm, *ps, *pa;  // scratch for cut tiles: nwg * 2 * tile records
+};
+bool qce_f64_shape(int MP, int NP);
+int qce_f64_tile();
+long long qce_pack_f64all_bytes(int MP, int NP, int has_mean);
+hipError_t qce_launch_pack_f64all(int K, int M, int N, int MP, int NP, int has_mean, const double2* Linv,
+                                  const double2* W, const double2* q0, const double2* bvec, double* pack,
+                                  hipStream_t st);
+hipError_t qce_launch_est_f64(const QceF64Args& a, bool out_partial, hipStream_t st);
+hipError_t qce_launch_f64_to_f32(const double* a, float* b, long long n, hipStream_t st);
+hipError_t qce_launch_f32_to_f64(const float* a, double* b, long long n, hipStream_t st);
+
 // *flag |= (some y * y_scale is not exactly representable in fp16); n = doubles in y
 hipError_t qce_launch_y_exact(long long n, const double* y, double y_scale, int* flag, hipStream_t st);
 

@@ -67,7 +67,7 @@ class Gmm_nbit:
     (K,N) and ``covs_cplx`` (K,N,N) the channel-domain model.
     """
 
-    def __init__(self, *gmm_args, device=0, **gmm_kwargs):
+    def __init__(self, *gmm_args, device=0, precision="f64", **gmm_kwargs):
         if _SkGaussianMixture is not None:
             self.gm = _SkGaussianMixture(*gmm_args, **gmm_kwargs)
         else:
@@ -80,6 +80,9 @@ class Gmm_nbit:
         self.params = dict()
         self.F2 = None
         self.device = device
+        # arithmetic of the dense 'all' mode: "f64" = the reference's complex128 (FP64 MFMA products and
+        # accumulation, the default), "fast" = fp16 two-term split products with fp32 accumulation (opt-in)
+        self.precision = precision
         self.mirror_state = True
         self._dev = None
         self._dev_key = None
@@ -99,9 +102,9 @@ class Gmm_nbit:
         return obj
 
     @classmethod
-    def from_params(cls, means_cplx, covs_cplx, weights, covariance_type="full", device=0):
+    def from_params(cls, means_cplx, covs_cplx, weights, covariance_type="full", device=0, precision="f64"):
         covs = np.asarray(covs_cplx, dtype=complex)
-        obj = cls(n_components=covs.shape[0], covariance_type=covariance_type, device=device)
+        obj = cls(n_components=covs.shape[0], covariance_type=covariance_type, device=device, precision=precision)
         obj.means_cplx = np.zeros(covs.shape[:2], complex) if means_cplx is None else np.asarray(means_cplx, complex)
         obj.covs_cplx = covs
         obj.gm.weights_ = np.asarray(weights, dtype=float)
@@ -218,9 +221,12 @@ class Gmm_nbit:
         covs = np.asarray(self.covs_cplx)
         means = self.means_cplx
         w = np.asarray(self.gm.weights_, dtype=float)
-        key = (id(self.covs_cplx), id(means), id(self.gm.weights_), covs.shape, self.device)
+        precision = getattr(self, "precision", "f64")
+        key = (id(self.covs_cplx), id(means), id(self.gm.weights_), covs.shape, self.device, precision)
         if self._dev is None or self._dev_key != key:
             self._dev = _lib.DeviceModel(means, covs, w, device=self.device)
+            if precision != "f64":
+                self._dev.set_precision(precision)
             self._dev_key = key
             self._state = None
         return self._dev
@@ -331,8 +337,8 @@ class Gmm_quant(Gmm_nbit):
     branch (:300-327): inf goes through the uniform-quantiser gain, which is the identity, so the
     result is the same; with a Lloyd quantiser the reference overflows, which is mirrored."""
 
-    def __init__(self, *gmm_args, device=0, **gmm_kwargs):
-        super().__init__(*gmm_args, device=device, **gmm_kwargs)
+    def __init__(self, *gmm_args, device=0, precision="f64", **gmm_kwargs):
+        super().__init__(*gmm_args, device=device, precision=precision, **gmm_kwargs)
         self.quantizer = None
         self.sigma2 = None
         self.n_bits = None
