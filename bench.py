@@ -5,23 +5,26 @@ A step is one ``estimate_from_y`` of the reference (gmm_cplx_bussgang.py:166-243
 the per-SNR FP64 precompute (prepare) followed by the fused estimate kernel, with the batch of
 quantised observations already resident in HBM.  Default workload = the metric configuration
 (SURVEY.md §8(d) D2): K=128 components, N=M=64 antennas, 'full' covariances, 1-bit uniform
-quantiser, SNR 5 dB, mode 'all', B=100,000 observations per GPU.
+quantiser, SNR 5 dB, mode 'all', B=100,000 observations, FP64 arithmetic (the reference's complex128).
 
   python bench.py [--gpus N --steps K --warmup W] [--config metric|cfg1..cfg5|cfg3dense|cfg5dense]
-                  [--shard batch|k]
+                  [--shard batch|k] [--precision f64|fast] [--chunks C]
 
-cfg3 / cfg5 are (block-)circulant mixtures with A = I: they take the Fourier-domain path
-(qce_fft.hip, HBM-bound roofline); the *dense variants force the dense path (QCE_FFT=0).
-
-Multi-GPU (launched by torch.distributed.run, one rank per GPU): ``--shard batch`` (default) gives
-every rank its own B observations and the whole mixture (no data-path collective, weak scaling);
-``--shard k`` splits the K components over the ranks and combines with one RCCL all-reduce
-(strong scaling).  Rank 0 prints one JSON line.
+Multi-GPU: one process per GPU.  ``--gpus N`` without a torch.distributed launcher starts the N ranks
+itself (child processes, before any GPU call); under ``torch.distributed.run`` the ranks come from the
+environment and must number ``--gpus``.  ``--shard k`` (default for the dense configs: metric, cfg1,
+cfg2, cfg4) splits the K components over the ranks (strong scaling: the B observations are estimated
+once by the whole node) and sums the shifted FP64 partials with one RCCL reduce-scatter per batch
+chunk, pipelined behind the next chunk's kernel; ``--shard batch`` (default for the
+Fourier paths cfg3 / cfg5) gives every rank its own B observations and the whole mixture (no
+data-path collective, weak scaling).  Rank 0 prints one JSON line.
 """
 import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -31,8 +34,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "channel estimates/sec + MSE vs reference; K=128 N=64 full-cov, 1/2/4/8 GPU"
-FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
 FP64_MFMA_PEAK_TFLOPS = 78.6  # MI355X_MICROARCH.md / SURVEY D3: v_mfma_f64_16x16x4_f64 dense peak (spec)
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak (spec)
 FP16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense FP16/BF16 MFMA (spec, no sparsity)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec (6.3 TB/s measured copy)
 
@@ -48,6 +51,8 @@ CONFIGS = {
     "cfg5dense": dict(K=128, N=256, cov="block-circulant", blocks=(4, 64), n_bits=2, qtype="uniform", B=100_000,
                       snr=5.0, dense=True),
 }
+DEFAULT_SHARD = {"metric": "k", "cfg1": "k", "cfg2": "k", "cfg4": "k", "cfg3": "batch", "cfg3dense": "batch",
+                 "cfg5": "batch", "cfg5dense": "batch"}
 
 
 def parse():
@@ -56,17 +61,60 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
-    ap.add_argument("--batch", type=int, default=0, help="override B (observations per GPU)")
-    ap.add_argument("--shard", default="batch", choices=["batch", "k"])
+    ap.add_argument("--batch", type=int, default=0, help="override B (observations per step)")
+    ap.add_argument("--shard", default=None, choices=["batch", "k"])
     ap.add_argument("--precision", default="f64", choices=["f64", "fast"],
-                    help="dense 'all' arithmetic: f64 (reference complex128, default) or fast (fp16 split)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline budget (0 = skip)")
+                    help="dense 'all' arithmetic: f64 (the reference's complex128, default) or fast (fp16 split)")
+    ap.add_argument("--chunks", type=int, default=4, help="K-shard pipeline chunks per batch")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--collective", default="rs", choices=["rs", "ar"],
+                    help="K-shard SUM collective: reduce-scatter (rank keeps its rows) or all-reduce")
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline budget per leg (0 = skip)")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the fast-path and drop-in side lines")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_metric.json"),
                     help="JSON with PMC-derived HBM bytes per launch of the estimate kernel")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.shard is None:
+        a.shard = DEFAULT_SHARD[a.config]
+    return a
 
 
+# ------------------------------------------------------------------------------------------ launcher
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n):
+    """Start n ranks of this script (one per GPU) before anything touches the GPU; exit with the worst
+    status.  A rank that fails takes the others down (their PIDs, not a pattern)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0:
+                rc = rc or c
+                for q in live:
+                    q.kill()
+        time.sleep(0.05)
+    return rc
+
+
+# ------------------------------------------------------------------------------------------ inputs
 def make_inputs(cfg, seed, pool=2048):
     """Synthetic batch of the configured shape: SCM channels (a seeded pool of `pool` distinct
     channels, reused with fresh noise) -> quantised observations y = Q(h + n)."""
@@ -85,37 +133,185 @@ def make_inputs(cfg, seed, pool=2048):
     return means, covs, w, h, np.ascontiguousarray(y, dtype=np.complex128), quantizer
 
 
-def cpu_baseline(cfg, means, covs, w, y, quantizer, budget_s):
-    """Loop-faithful oracle (the reference's per-(sample, component) op order) on a bounded
-    sample of the same workload, single thread."""
-    from oracle import qce_oracle as O
+# ------------------------------------------------------------------------------------------ CPU baseline
+def _cpu_model():
     try:
-        from threadpoolctl import threadpool_limits
-        lim = threadpool_limits(limits=1)
-    except Exception:  # pragma: no cover
-        lim = None
-    N = cfg["N"]
-    def run(n):
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _pool_worker(args):
+    """One Pool worker: the loop-faithful oracle on its shard, single-threaded BLAS (the reference's
+    mp_gmm worker, Bussgang_GMM.py:16-17, one estimate_from_y per task incl. its prepare)."""
+    from threadpoolctl import threadpool_limits
+    from oracle import qce_oracle as O
+    means, covs, w, y, snr, N, n_bits, qtype, quantizer = args
+    with threadpool_limits(limits=1):
         t0 = time.perf_counter()
-        O.estimate_loop(means, covs, w, y[:n], cfg["snr"], N, None, cfg["n_bits"], cfg["qtype"], quantizer)
+        O.estimate_loop(means, covs, w, y, snr, N, None, n_bits, qtype, quantizer)
         return time.perf_counter() - t0
-    a, b = (4, 36) if N <= 64 else (1, 3)  # N >= 128: one loop-faithful estimate costs ~0.1-2 s
-    t1, t2 = run(a), run(b)
-    per = max((t2 - t1) / (b - a), 1e-6)
-    prep = max(t1 - a * per, 0.0)
-    n = int(max(b, min(y.shape[0], (budget_s - prep) / per)))
+
+
+def cpu_baseline(cfg, means, covs, w, y, quantizer, budget_s):
+    """The reference's CPU path timed on this host: the loop-faithful restatement
+    (same per-(sample, component) op order as gmm_cplx_bussgang.py:223-228 incl. the redundant
+    C_k A_eff^H) (i) in one process, one BLAS thread, (ii) in a Pool of cpu_count()//2 single-thread
+    workers sharding the batch, as Bussgang_GMM.py:29-32 sizes its pool (capped at the 16 host cores
+    a one-GPU box grants), and (iii) the vectorised FP64 oracle ("optimised CPU", BLAS threads = the
+    pool size).  Bounded samples: the cost is linear in B (per-call prepare included)."""
+    import multiprocessing as mp
+    from threadpoolctl import threadpool_limits
+    from oracle import qce_oracle as O
+    N, snr, nb, qt = cfg["N"], cfg["snr"], cfg["n_bits"], cfg["qtype"]
+    nproc = os.cpu_count() or 1
+    npool = max(1, min(nproc // 2, 16))
+
+    def loop(n):
+        t0 = time.perf_counter()
+        O.estimate_loop(means, covs, w, y[:n], snr, N, None, nb, qt, quantizer)
+        return time.perf_counter() - t0
+
+    with threadpool_limits(limits=1):
+        a, b = (4, 24) if N <= 64 else (1, 3)
+        t1, t2 = loop(a), loop(b)
+        per = max((t2 - t1) / (b - a), 1e-6)
+        prep = max(t1 - a * per, 0.0)
+        n1 = int(max(b, min(y.shape[0], (budget_s - prep) / per)))
+        dt1 = loop(n1)
+    single = dict(value=round(n1 / dt1, 2), cores=1, sample=f"{n1} observations, {dt1:.1f} s (prepare included)")
+    # (ii) process pool, one shard per worker
+    nper = int(max(2, min(y.shape[0] // npool, (budget_s - prep) / per)))
+    tasks = [(means, covs, w, y[i * nper:(i + 1) * nper], snr, N, nb, qt, quantizer) for i in range(npool)]
+    ctx = mp.get_context("fork")
+    with ctx.Pool(npool) as pool:
+        t0 = time.perf_counter()
+        pool.map(_pool_worker, tasks, chunksize=1)
+        dtp = time.perf_counter() - t0
+    pooled = npool * nper / dtp
+    # (iii) vectorised oracle
+    with threadpool_limits(limits=npool):
+        nv = min(y.shape[0], 2000 if N <= 64 else 400)
+        t0 = time.perf_counter()
+        O.estimate(means, covs, w, y[:nv], snr, N, None, "all", nb, qt, quantizer)
+        dtv = time.perf_counter() - t0
+    return dict(value=round(pooled, 2), unit="channel estimates/s", cores=npool, kind="port",
+                sample=f"Pool({npool}) of single-thread workers (Bussgang_GMM.py:29-32 sizing, capped at 16), "
+                       f"{nper} observations each through oracle.estimate_loop (per-call prepare included), "
+                       f"{dtp:.1f} s wall",
+                nproc=nproc, cpu_model=_cpu_model(), single_process=single,
+                vectorised=dict(value=round(nv / dtv, 2), cores=npool,
+                                sample=f"{nv} observations through oracle.estimate (vectorised FP64), {dtv:.2f} s"))
+
+
+# ------------------------------------------------------------------------------------------ roofline
+def f64_executed_flops(N, K, B):
+    """Executed v_mfma_f64_16x16x4 work of k_est_all_f64: 256 flops per sample per 1 KB table block
+    (GL: NTL(NTL+1) blocks — Linv's upper triangle skipped; GW: NTW*KP blocks)."""
+    Np = 16 if N <= 16 else (32 if N <= 32 else 64)
+    ntl, ntw, kp = Np // 8, Np // 8, Np // 4
+    return 256.0 * (ntl * (ntl + 1) + ntw * kp) * K * B
+
+
+def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
+    N = cfg["N"]
+    fourier = bool(dm.structure()[2])
+    if fourier:
+        # HBM-bound (SURVEY §8(d) D3): 16 M bytes of y in + 16 N bytes of h out per estimate (c128)
+        bytes_per_launch = 32.0 * N * B
+        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        n1, n2, _ = dm.structure()
+        fft_flops = (4.0 * k_local * N + 10.0 * N * math.log2(N)) * B  # D3: zero-mean FFT-path flops
+        return dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
+                    kernel="k_fft_mfma", structure=f"block-circulant ({n1},{n2})" if n1 > 1 else "circulant",
+                    kernel_ms=round(kern_ms, 4), bytes_per_launch=bytes_per_launch,
+                    fp64_flops_per_launch=fft_flops, fp64_tflops=round(fft_flops / (kern_ms * 1e-3) / 1e12, 3))
+    flops = 16.0 * k_local * N * N * B  # SURVEY §8(d) D3: 16 K M N real flops per estimate
+    achieved = flops / (kern_ms * 1e-3) / 1e12
+    if dm.precision == "f64" and N <= 64:
+        ex = f64_executed_flops(N, k_local, B)
+        return dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
+                    frac=round(achieved / FP64_MFMA_PEAK_TFLOPS, 4), traffic=traffic,
+                    kernel="k_est_all_f64 (+k_merge_f64)", peak_dtype="fp64 MFMA (dense)",
+                    kernel_ms=round(kern_ms, 4), flops_per_launch=flops, executed_flops_per_launch=ex,
+                    mfma_issue_frac=round(ex / (kern_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
+                    note="algorithmic flops (16KMN) / time; frac can exceed 1 because the upper triangle of "
+                         "Linv is skipped (executed = 0.78 of algorithmic at N=64): mfma_issue_frac is the "
+                         "executed-MFMA fraction of the FP64 peak")
+    nsl = (2 * N) // 32
+    tri = (sum(2 * r + 2 for r in range(nsl)) / (nsl * 2 * nsl) + 1.0) / 2.0
+    ex = flops * tri * 2.0
+    return dict(bound="mfma", achieved=round(achieved, 3), peak=FP16_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
+                frac=round(achieved / FP16_MFMA_PEAK_TFLOPS, 4), traffic=traffic,
+                kernel="k_est_all_h2 / k_est_all_h2x", peak_dtype="fp16 MFMA (dense)",
+                kernel_ms=round(kern_ms, 4), flops_per_launch=flops,
+                mfma_issue_frac=round(ex / (kern_ms * 1e-3) / 1e12 / FP16_MFMA_PEAK_TFLOPS, 4))
+
+
+def dtype_of(dm):
+    if dm.structure()[2]:
+        return "f64"
+    if dm.precision == "f64" and dm.N <= 64:
+        return "f64"
+    return "f16x2 (fp16 hi+lo split, fp32 accumulate, fp64 softmax)"
+
+
+# ------------------------------------------------------------------------------------------ side lines
+def fast_line(cfg, means, covs, w, yd, out, stream, steps, qargs, ho, n_chk):
+    """The opt-in fast path (fp16 two-term split, fp32 accumulate) on the same workload: its own
+    throughput and parity, reported beside the FP64 headline (never as `value`)."""
+    import torch
+    from quantized_channel_estimation_amd import _lib
+    dm = _lib.DeviceModel(means, covs, w)
+    dm.set_precision("fast")
+    sptr = stream.cuda_stream
+    for _ in range(2):
+        dm.prepare(None, cfg["snr"], cfg["n_bits"], *qargs, stream=sptr)
+        dm.estimate(yd, _lib.MODE_ALL, 0.0, out=out, stream=sptr)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     t0 = time.perf_counter()
-    O.estimate_loop(means, covs, w, y[:n], cfg["snr"], N, None, cfg["n_bits"], cfg["qtype"], quantizer)
+    for i in range(steps):
+        dm.prepare(None, cfg["snr"], cfg["n_bits"], *qargs, stream=sptr)
+        ev[i][0].record(stream)
+        dm.estimate(yd, _lib.MODE_ALL, 0.0, out=out, stream=sptr)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    if lim is not None:
-        lim.unregister()
-    return dict(value=n / dt, unit="estimates/s", cores=1, kind="port",
-                sample=f"{n} observations of the same workload through oracle.estimate_loop (per-call prepare "
-                       f"included, 1 BLAS thread), {dt:.1f} s")
+    kms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    hg = out[:n_chk].cpu().numpy()
+    res = dict(value=round(yd.shape[0] * steps / dt, 1), ms_per_step=round(dt / steps * 1e3, 4),
+               kernel_ms=round(kms, 4), dtype=dtype_of(dm))
+    if ho is not None:
+        res["parity_rel_fro"] = float(np.linalg.norm(hg - ho) / np.linalg.norm(ho))
+    dm.close()
+    return res
 
 
+def dropin_line(cfg, means, covs, w, y, quantizer, calls=3):
+    """The drop-in API as the scripts call it: Gmm_nbit.estimate_from_y with numpy y in and numpy h out
+    (H2D + prepare + kernel + D2H, reference state mirroring deferred until gm is read)."""
+    from quantized_channel_estimation_amd import Gmm_nbit
+    g = Gmm_nbit.from_params(means, covs, w)
+    args = (cfg["snr"], cfg["N"], None, "all", cfg["n_bits"], cfg["qtype"], quantizer)
+    g.estimate_from_y(y, *args)
+    t0 = time.perf_counter()
+    for _ in range(calls):
+        g.estimate_from_y(y, *args)
+    dt = (time.perf_counter() - t0) / calls
+    return dict(value=round(y.shape[0] / dt, 1), ms_per_call=round(dt * 1e3, 3), calls=calls,
+                io="host numpy complex128 in/out, state mirror lazy")
+
+
+# ------------------------------------------------------------------------------------------ main
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     cfg = dict(CONFIGS[args.config])
     if cfg.pop("dense", False):
         os.environ["QCE_FFT"] = "0"  # read by qce_prepare: keep the structured mixture on the dense path
@@ -126,18 +322,32 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    # ranks beyond the visible GPUs share them (single-GPU rehearsals of the multi-rank path; on a node
+    # with one GPU per rank this is the identity).  device_count() does not initialise the GPU.
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     if args.batch:
         cfg["B"] = args.batch
     K, N, B = cfg["K"], cfg["N"], cfg["B"]
     data_seed = rank if args.shard == "batch" else 0
     means, covs, w, h, y, quantizer = make_inputs(cfg, data_seed)
+    # the CPU baseline runs first, before this process touches the GPU (its Pool forks workers)
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(cfg, means, covs, w, y, quantizer, args.cpu_seconds)
+    torch.cuda.set_device(local)
+    if world > 1:
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
+        world = dist.get_world_size()
+    kshard = args.shard == "k" and world > 1
     qkind = {"uniform": _lib.QUANT_UNIFORM, "lloyd": _lib.QUANT_LLOYD}[cfg["qtype"]]
     thr, lab = (quantizer[0], quantizer[1]) if cfg["n_bits"] not in (1, np.inf) and cfg["qtype"] == "lloyd" else \
         (None, None)
+    qargs = (qkind, thr, lab)
 
     dev = torch.device("cuda", local)
     yd = torch.from_numpy(y).to(dev)
@@ -146,34 +356,41 @@ def main():
     torch.cuda.set_stream(stream)
     sptr = stream.cuda_stream
 
-    if args.shard == "batch":
+    if not kshard:
         model = _lib.DeviceModel(means, covs, w, device=local)
         if args.precision != "f64":
             model.set_precision(args.precision)
+        dm = model
 
         def step(ev=None):
-            model.prepare(None, cfg["snr"], cfg["n_bits"], qkind, thr, lab, stream=sptr)
+            model.prepare(None, cfg["snr"], cfg["n_bits"], *qargs, stream=sptr)
             if ev is not None:
-                ev[0].record(stream)
+                ev[0][0].record(stream)
             model.estimate(yd, _lib.MODE_ALL, 0.0, out=out, stream=sptr)
             if ev is not None:
-                ev[1].record(stream)
-            return out
+                ev[0][1].record(stream)
+            return None, out
     else:
-        shard = ComponentShardEstimator(means, covs, w, rank, world, device=local)
-        m_b = torch.empty(B, dtype=torch.float64, device=dev)
-        s_b = torch.empty(B, dtype=torch.float64, device=dev)
-        a_b = torch.empty((B, 2 * N), dtype=torch.float32, device=dev)
-        from quantized_channel_estimation_amd.sharding import combine_partials_dist
+        shard = ComponentShardEstimator(means, covs, w, rank, world, device=local, precision=args.precision)
+        dm = shard.dev
+        # time only the partial kernels on the compute stream (the collectives run on RCCL's stream)
+        orig = shard.dev.partial_shifted
 
         def step(ev=None):
-            shard.prepare(None, cfg["snr"], cfg["n_bits"], qkind, thr, lab, stream=sptr)
+            shard.prepare(None, cfg["snr"], cfg["n_bits"], *qargs, stream=sptr)
             if ev is not None:
-                ev[0].record(stream)
-            shard.dev.partial(yd, m_b, s_b, a_b, stream=sptr)
-            if ev is not None:
-                ev[1].record(stream)
-            return combine_partials_dist(m_b, s_b, a_b, shard.shift, N)
+                def timed(*a, **kw):
+                    e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    ev.append(e)
+                    e[0].record(stream)
+                    r = orig(*a, **kw)
+                    e[1].record(stream)
+                    return r
+                shard.dev.partial_shifted = timed
+            try:
+                return shard.estimate(yd, chunks=args.chunks, scatter=args.collective == "rs")
+            finally:
+                shard.dev.partial_shifted = orig
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -183,44 +400,48 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if kshard:
+        events = [[] for _ in range(args.steps)]  # filled per chunk by the timed partial launches
+    else:
+        events = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
+                  for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
         res = step(events[i])
     barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    kern_ms = float(np.mean([sum(a.elapsed_time(b) for a, b in evs) for evs in events]))
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
     ms_per_step = elapsed / args.steps * 1e3
-    total_units = B * world if args.shard == "batch" else B
+    total_units = B if kshard else B * world  # K-shard: the node estimates B once; batch: B per rank
     value = total_units * args.steps / elapsed
 
     # parity + MSE of this rank's last result against the FP64 oracle on a subset
-    parity = None
-    mse = None
+    parity = mse = None
+    ho = None
+    n_chk = min(B, 512)
+    rows, hres = res
     if rank == 0:
-        hg = res.cpu().numpy()
-        mse = float(np.mean(np.abs(hg - h) ** 2))
+        hg = hres.cpu().numpy()
+        idx = np.arange(B) if rows is None else rows.cpu().numpy()
+        mse = float(np.mean(np.abs(hg - h[idx]) ** 2))
         if not args.no_parity:
             from oracle import qce_oracle as O
-            n_chk = min(B, 512)
-            ho = O.estimate(means, covs, w, y[:n_chk], cfg["snr"], N, None, "all", cfg["n_bits"], cfg["qtype"],
+            sel = idx[:n_chk]
+            ho = O.estimate(means, covs, w, y[sel], cfg["snr"], N, None, "all", cfg["n_bits"], cfg["qtype"],
                             quantizer)
-            parity = dict(samples=n_chk,
+            parity = dict(samples=int(sel.size),
                           rel_fro=float(np.linalg.norm(hg[:n_chk] - ho) / np.linalg.norm(ho)),
-                          mse_gpu=float(np.mean(np.abs(hg[:n_chk] - h[:n_chk]) ** 2)),
-                          mse_oracle=float(np.mean(np.abs(ho - h[:n_chk]) ** 2)))
+                          mse_gpu=float(np.mean(np.abs(hg[:n_chk] - h[sel]) ** 2)),
+                          mse_oracle=float(np.mean(np.abs(ho - h[sel]) ** 2)))
 
-    # roofline of the dominant kernel
-    k_local = K if args.shard == "batch" else (lambda s: s[1] - s[0])(component_slices(K, world)[rank])
-    dm = model if args.shard == "batch" else shard.dev
-    fourier = bool(dm.structure()[2])
-    f32_kernel = os.environ.get("QCE_KERNEL") == "f32"
+    # roofline of the dominant kernel (per rank)
+    k_local = (lambda s: s[1] - s[0])(component_slices(K, world)[rank]) if kshard else K
+    kern_tag = "fft" if dm.structure()[2] else ("f64" if dtype_of(dm) == "f64" else "h2")
     traffic = None
-    kern_tag = "fft" if fourier else ("f32" if f32_kernel else "h2")
     if os.path.exists(args.traffic):
         try:
             tj = json.load(open(args.traffic))
@@ -228,76 +449,41 @@ def main():
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    if fourier:
-        # HBM-bound: 16 M bytes of y in + 16 N bytes of h out per estimate (c128)
-        bytes_per_launch = 32.0 * N * B
-        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-        n1, n2, _ = dm.structure()
-        fft_flops = (4.0 * k_local * N + 10.0 * N * math.log2(N)) * B  # D3: zero-mean FFT-path flops
-        roofline = dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
-                        kernel="k_fft_est", structure=f"block-circulant ({n1},{n2})" if n1 > 1 else "circulant",
-                        kernel_ms=round(kern_ms, 4), bytes_per_launch=bytes_per_launch,
-                        fp64_flops_per_launch=fft_flops,
-                        fp64_tflops=round(fft_flops / (kern_ms * 1e-3) / 1e12, 3))
-    else:
-        flops_per_launch = 16.0 * k_local * N * N * B  # 16 K M N real flops / estimate
-        achieved = flops_per_launch / (kern_ms * 1e-3) / 1e12
-        if args.precision == "f64" and not f32_kernel and N <= 64:
-            # FP64 kernel: executed v_mfma_f64_16x16x4 work = 256 flops per sample per 1 KB table block
-            # (GL: NTL(NTL+1) blocks, Linv's upper triangle skipped; GW: NTW * KP blocks)
-            Np = 16 if N <= 16 else (32 if N <= 32 else 64)
-            ntl, ntw, kp = Np // 8, Np // 8, Np // 4
-            executed = 256.0 * (ntl * (ntl + 1) + ntw * kp) * k_local * B
-            roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
-                            frac=round(achieved / FP64_MFMA_PEAK_TFLOPS, 4), traffic=traffic,
-                            kernel="k_est_all_f64 (+k_merge_f64)", peak_dtype="fp64 MFMA (dense)",
-                            kernel_ms=round(kern_ms, 4), flops_per_launch=flops_per_launch,
-                            executed_flops_per_launch=executed,
-                            mfma_issue_frac=round(executed / (kern_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4))
-        peak = FP32_MFMA_PEAK_TFLOPS if f32_kernel else FP16_MFMA_PEAK_TFLOPS
-        # executed MFMA work: lower-triangular tiles of E(Linv) skipped (R/32 slices of 32x16 tiles) and,
-        # for the fp16 kernel, two products (hi, lo) per fp32-class MAC
-        nsl = (2 * N) // 32
-        tri = (sum(2 * r + 2 for r in range(nsl)) / (nsl * 2 * nsl) + 1.0) / 2.0
-        executed = flops_per_launch * tri * (1.0 if f32_kernel else 2.0)
-        if not (args.precision == "f64" and not f32_kernel and N <= 64):
-          roofline = dict(bound="mfma", achieved=round(achieved, 3), peak=peak, unit="TFLOP/s",
-                        frac=round(achieved / peak, 4), traffic=traffic,
-                        kernel=("k_est_all_f32" if f32_kernel else "k_est_all_h2+k_merge_streamk"),
-                        peak_dtype="fp32 MFMA" if f32_kernel else "fp16 MFMA (dense)",
-                        kernel_ms=round(kern_ms, 4), flops_per_launch=flops_per_launch,
-                        mfma_issue_frac=round(executed / (kern_ms * 1e-3) / 1e12 / peak, 4))
+    roofline = roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic)
 
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(cfg, means, covs, w, y, quantizer, args.cpu_seconds)
-
+    extras = {}
+    if rank == 0 and world == 1 and not args.no_extras and args.config == "metric":
+        extras["fast_path"] = fast_line(cfg, means, covs, w, yd, out, stream, max(3, args.steps // 2), qargs, ho,
+                                        n_chk)
+        extras["dropin"] = dropin_line(cfg, means, covs, w, y, quantizer)
     if rank == 0:
         line = {
             "metric": METRIC,
             "value": round(value, 1),
             "unit": "channel estimates/s",
             "n_gpus": world,
+            "world_size": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak" if args.shard == "batch" else "strong",
+            "scaling": "strong" if args.shard == "k" else "weak",
             "vs_baseline": None,
-            "dtype": "f64" if (fourier or (args.precision == "f64" and not f32_kernel and N <= 64)) else (
-                "f32" if f32_kernel else "f16x2 (fp16 hi+lo split, fp32 accumulate, fp64 softmax)"),
+            "dtype": dtype_of(dm),
             "data": f"synthetic: seeded {cfg['cov']} SCM-derived covariances, SCM channel pool + fresh CN noise, "
                     f"{cfg['n_bits']}-bit {cfg['qtype']} quantised",
             "config": {"workload": f"estimate_from_y K={K} N=M={N} cov={cfg['cov']} n_bits={cfg['n_bits']} "
-                                   f"{cfg['qtype']} snr={cfg['snr']}dB mode=all B={B}/GPU prepare-per-step",
-                       "K": K, "N": N, "B_per_gpu": B, "shard": args.shard,
-                       "parallelism": f"{args.shard}{world}"},
+                                   f"{cfg['qtype']} snr={cfg['snr']}dB mode=all B={B}"
+                                   f"{'' if args.shard == 'k' else '/GPU'} prepare-per-step",
+                       "K": K, "N": N, "B": B, "shard": args.shard,
+                       "parallelism": f"{'kshard' if args.shard == 'k' else 'batch'}{world}",
+                       "chunks": args.chunks if kshard else None},
             "mse": mse,
             "parity": parity,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        line.update(extras)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

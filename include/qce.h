@@ -107,6 +107,14 @@ int qce_estimate_partial(qce_model* model, const double* y, int64_t B, double* m
 int qce_estimate_partial_f64(qce_model* model, const double* y, int64_t B, double* m_out, double* s_out, double* acc_out,
                              int io, void* stream);
 
+/* The K-shard partial scaled to a shift shared by all shards and packed for one SUM collective:
+ * packed_out (B, 2N+2) f64, row b = [s_b e^{m_b - shift}, 0, acc_b e^{m_b - shift} (2N interleaved)].
+ * With shift = max over ALL components of cconst (>= every lp, the quad form is >= 0) the element-wise sum
+ * over shards of these rows gives h_b = acc / s exactly (rows whose sum underflows to s = 0 need the
+ * two-step combine of the unshifted partials). */
+int qce_estimate_partial_shifted(qce_model* model, const double* y, int64_t B, double shift, double* packed_out, int io,
+                                 void* stream);
+
 /* Per-SNR tables for state mirroring (the reference mutates gm.means_, gm.covariances_,
  * gm.precisions_cholesky_, :262-313) and tests.  Host pointers, any may be NULL:
  * means_y (K,M), Cy (K,M,M), Cr (K,M,M), P (K,M,M) = (L^-1)^H, A_eff (K,M,N), W (K,N,M),

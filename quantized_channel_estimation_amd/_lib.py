@@ -51,6 +51,8 @@ SIGNATURES = {
     "qce_log_prob": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int, _vp]),
     "qce_estimate_partial": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int, _vp]),
     "qce_estimate_partial_f64": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int, _vp]),
+    "qce_estimate_partial_shifted": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_double, _vp, ctypes.c_int,
+                                                    _vp]),
     "qce_get_tables": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "qce_model_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                       ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
@@ -270,6 +272,28 @@ class DeviceModel:
         self._order_after(io, stream)
         return m_out, s_out, acc_out
 
+    def partial_shifted(self, y, shift, out=None, stream=None):
+        """Shifted packed K-shard partial (qce_estimate_partial_shifted): (B, 2N+2) f64 rows
+        [s e^{m-shift}, 0, acc e^{m-shift}] that sum over shards."""
+        io = IO_HOST if isinstance(y, np.ndarray) else IO_DEVICE
+        B = y.shape[0]
+        if io == IO_HOST:
+            y = np.ascontiguousarray(y, dtype=np.complex128)
+            out = np.empty((B, 2 * self.N + 2)) if out is None else out
+        elif out is None:
+            import torch
+            out = torch.empty((B, 2 * self.N + 2), dtype=torch.float64, device=y.device)
+        self._order_before(y, io, stream)
+        check(load().qce_estimate_partial_shifted(self._h, ptr(y), int(B), float(shift), ptr(out), io, stream))
+        self._order_after(io, stream)
+        return out
+
+    def cconst(self):
+        """c_k = -M log(pi) + 2 log det P_k + log w_k of the last prepare (K,) — the shard shift input."""
+        c = np.empty(self.K)
+        check(load().qce_get_tables(self._h, None, None, None, None, None, None, None, ptr(c)))
+        return c
+
     def set_precision(self, precision):
         """'f64' (default: the reference's complex128 arithmetic) or 'fast' (fp16 two-term split products,
         fp32 accumulation) for the dense 'all' mode and the K-shard partial."""
@@ -298,13 +322,16 @@ class DeviceModel:
         check(fn(self._h, ptr(y), int(B), ptr(c), ptr(out), IO_HOST, None))
         return out
 
-    def tables(self):
+    _TABLES = ("means_y", "Cy", "Cr", "P", "A_eff", "W", "b", "cconst")
+
+    def tables(self, names=None):
+        """Per-SNR tables of the last prepare (qce_get_tables); `names` restricts the copy."""
         K, M, N = self.K, self.M, self.N
-        t = dict(means_y=np.empty((K, M), complex), Cy=np.empty((K, M, M), complex), Cr=np.empty((K, M, M), complex),
-                 P=np.empty((K, M, M), complex), A_eff=np.empty((K, M, N), complex), W=np.empty((K, N, M), complex),
-                 b=np.empty((K, N), complex), cconst=np.empty(K))
-        check(load().qce_get_tables(self._h, *(ptr(t[k]) for k in ("means_y", "Cy", "Cr", "P", "A_eff", "W", "b",
-                                                                    "cconst"))))
+        shapes = dict(means_y=(K, M), Cy=(K, M, M), Cr=(K, M, M), P=(K, M, M), A_eff=(K, M, N), W=(K, N, M),
+                      b=(K, N), cconst=(K,))
+        names = self._TABLES if names is None else tuple(names)
+        t = {k: np.empty(shapes[k], float if k == "cconst" else complex) for k in names}
+        check(load().qce_get_tables(self._h, *(ptr(t.get(k)) for k in self._TABLES)))
         return t
 
     def synchronize(self):

@@ -98,6 +98,7 @@ struct qce_model {
   int f64_active = 0;  // the last dense prepare packed FP64 tables: 'all' / partial run k_est_all_f64
   DevBuf<double> fp_m, fp_s, fp_a;
   DevBuf<double> part_a64;  // FP64 partial accumulator behind the f32 qce_estimate_partial
+  DevBuf<double> fp_pack;   // host-I/O staging of qce_estimate_partial_shifted
   int cu_count = 256;
   // Fourier-domain path for (block-)circulant mixtures (qce_fft.hip): structure found at creation
   int fft_n1 = 0, fft_n2 = 0;
@@ -186,7 +187,7 @@ bool want_f64(const qce_model* m) {
 // per CU, the remaining tiles' (tile, component) items dealt out stream-K; final h, or the FP64
 // (m, s, acc) partial when h == nullptr (K-shard path)
 int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, double* oa,
-            hipStream_t st) {
+            hipStream_t st, double* pk = nullptr, double shift = 0.0) {
   const long long TS = qce_f64_tile();
   const long long tiles = (B + TS - 1) / TS;
   long long slots = m->cu_count;  // 128 KB of LDS: one workgroup per CU
@@ -227,6 +228,8 @@ int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om
   a.pm = m->fp_m.p;
   a.ps = m->fp_s.p;
   a.pa = m->fp_a.p;
+  a.pk = pk;
+  a.shift = shift;
   HIPCHK(qce_launch_est_f64(a, h == nullptr, st));
   return QCE_OK;
 }
@@ -540,7 +543,7 @@ int qce_model_destroy(qce_model* m) {
   m->sp_a.release();
   m->yflag.release();
   m->pack_f64.release();
-  for (auto* b : {&m->fp_m, &m->fp_s, &m->fp_a, &m->part_a64}) b->release();
+  for (auto* b : {&m->fp_m, &m->fp_s, &m->fp_a, &m->part_a64, &m->fp_pack}) b->release();
   for (auto* b : {&m->f_ceig, &m->f_rinvT, &m->f_cprime, &m->f_wT, &m->f_gain}) b->release();
   for (auto* b : {&m->f_col0, &m->f_mspec, &m->f_uT, &m->f_bT}) b->release();
   m->f_bad.release();
@@ -1055,6 +1058,40 @@ int qce_estimate_partial_f64(qce_model* m, const double* y, int64_t B, double* m
     HIPCHK(hipMemcpyAsync(m_out, dm, sizeof(double) * B, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(s_out, ds, sizeof(double) * B, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(acc_out, da, sizeof(double) * (size_t)B * 2 * m->N, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }
+  return QCE_OK;
+}
+
+int qce_estimate_partial_shifted(qce_model* m, const double* y, int64_t B, double shift, double* packed_out, int io,
+                                 void* stream) {
+  int rc = check_model(m, true);
+  if (rc) return rc;
+  if (B < 0 || (B > 0 && (!y || !packed_out))) return fail(QCE_EARG, "bad arguments");
+  if (B == 0) return QCE_OK;
+  DeviceGuard g(m->device);
+  hipStream_t st = pick_stream(m, stream);
+  const double2* dy = nullptr;
+  if ((rc = stage_input(m, y, B, io, st, &dy))) return rc;
+  const size_t W = (size_t)B * (2 * m->N + 2);
+  double* dp = packed_out;
+  if (io == QCE_IO_HOST) {
+    HIPCHK(m->fp_pack.ensure(W));
+    dp = m->fp_pack.p;
+  }
+  if (!m->fft_active && m->f64_active) {
+    if ((rc = run_f64(m, dy, B, nullptr, nullptr, nullptr, nullptr, st, dp, shift))) return rc;
+  } else {  // other paths: their (m, s, acc) partial, scaled and packed
+    HIPCHK(m->m_scr.ensure((size_t)B));
+    HIPCHK(m->s_scr.ensure((size_t)B));
+    HIPCHK(m->part_a64.ensure((size_t)B * 2 * m->N));
+    if ((rc = qce_estimate_partial_f64(m, reinterpret_cast<const double*>(dy), B, m->m_scr.p, m->s_scr.p,
+                                       m->part_a64.p, QCE_IO_DEVICE, st)))
+      return rc;
+    HIPCHK(qce_launch_pack_shifted(B, m->N, m->m_scr.p, m->s_scr.p, m->part_a64.p, nullptr, shift, dp, st));
+  }
+  if (io == QCE_IO_HOST) {
+    HIPCHK(hipMemcpyAsync(packed_out, dp, sizeof(double) * W, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
   }
   return QCE_OK;

@@ -138,7 +138,8 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
                                                          const double* __restrict__ cconst, double2* __restrict__ h,
                                                          double* __restrict__ om, double* __restrict__ os,
                                                          double* __restrict__ oa, double* __restrict__ pm,
-                                                         double* __restrict__ ps, double* __restrict__ pa) {
+                                                         double* __restrict__ ps, double* __restrict__ pa,
+                                                         double* __restrict__ pk, double shift) {
   using G = F64G<MP, NP, HM>;
   constexpr int TS = NW * 16 * CT;           // samples per tile
   constexpr int LPW = (F64_CHUNK / 1024) / NW;  // global_load_lds per wave per chunk
@@ -337,7 +338,17 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
       const bool whole = (klo == 0 && khi == K);
       const bool pfmt = OUT_PARTIAL || !whole;
       const long long row = whole ? sample : (w * 2 + (t == t_first ? 0 : 1)) * TS + ls;
-      if (pfmt) {
+      if (OUT_PARTIAL && whole && pk) {  // shifted packed partial: [s e^{m-M*}, 0, acc e^{m-M*}] (K-shard sum)
+        const double sc = (m[c] == QCE_NEG_INF) ? 0.0 : exp(m[c] - shift);
+        double* dp = pk + sample * (2LL * N + 2);
+        if (g == 0) *reinterpret_cast<double2*>(dp) = make_double2(ssum[c] * sc, 0.0);
+#pragma unroll
+        for (int T = 0; T < G::NTW; ++T) {
+          const int i0 = 8 * T + g, i1 = 8 * T + 4 + g;
+          if (i0 < N) *reinterpret_cast<double2*>(dp + 2 + 2 * i0) = make_double2(out[T][c][0] * sc, out[T][c][1] * sc);
+          if (i1 < N) *reinterpret_cast<double2*>(dp + 2 + 2 * i1) = make_double2(out[T][c][2] * sc, out[T][c][3] * sc);
+        }
+      } else if (pfmt) {
         double* dm = whole ? om : pm;
         double* ds = whole ? os : ps;
         double* da = (whole ? oa : pa) + row * (2LL * N);
@@ -372,7 +383,7 @@ __global__ __launch_bounds__(256) void k_merge_f64(long long B, int N, int K, in
                                                    const double* __restrict__ pm, const double* __restrict__ ps,
                                                    const double* __restrict__ pa, double2* __restrict__ h,
                                                    double* __restrict__ om, double* __restrict__ os,
-                                                   double* __restrict__ oa) {
+                                                   double* __restrict__ oa, double* __restrict__ pk, double shift) {
   const long long b = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (b >= B || L <= 0) return;
@@ -390,6 +401,7 @@ __global__ __launch_bounds__(256) void k_merge_f64(long long B, int N, int K, in
     const long long r = rec_of(w);
     s += (pm[r] == QCE_NEG_INF) ? 0.0 : ps[r] * exp(pm[r] - mx);
   }
+  const double psc = (pk && mx != QCE_NEG_INF) ? exp(mx - shift) : 0.0;  // shifted packed output
   for (int n = lane; n < N; n += 64) {
     double re = 0.0, im = 0.0;
     for (long long w = wa; w <= wb; ++w) {
@@ -401,14 +413,44 @@ __global__ __launch_bounds__(256) void k_merge_f64(long long B, int N, int K, in
     }
     if (h) {
       h[b * N + n] = make_double2(re / s, im / s);
+    } else if (pk) {
+      *reinterpret_cast<double2*>(pk + b * (2 * N + 2) + 2 + 2 * n) = make_double2(re * psc, im * psc);
     } else {
       *reinterpret_cast<double2*>(oa + b * 2 * N + 2 * n) = make_double2(re, im);
     }
   }
   if (!h && lane == 0) {
-    om[b] = mx;
-    os[b] = s;
+    if (pk) {
+      *reinterpret_cast<double2*>(pk + b * (2 * N + 2)) = make_double2(s * psc, 0.0);
+    } else {
+      om[b] = mx;
+      os[b] = s;
+    }
   }
+}
+
+// [m, s, acc] partial (acc f64, or f32 when acc32) -> shifted packed [s e^{m-M*}, 0, acc e^{m-M*}]
+__global__ __launch_bounds__(256) void k_pack_shifted(long long B, int N, const double* __restrict__ m,
+                                                      const double* __restrict__ s, const double* __restrict__ acc,
+                                                      const float* __restrict__ acc32, double shift,
+                                                      double* __restrict__ pk) {
+  const long long W = 2LL * N + 2;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < B * W; i += (long long)gridDim.x * 256) {
+    const long long b = i / W, j = i % W;
+    const double sc = (m[b] == QCE_NEG_INF) ? 0.0 : exp(m[b] - shift);
+    double v;
+    if (j == 0) v = s[b];
+    else if (j == 1) v = 0.0;
+    else v = acc32 ? (double)acc32[b * 2 * N + j - 2] : acc[b * 2 * N + j - 2];
+    pk[i] = v * sc;
+  }
+}
+hipError_t qce_launch_pack_shifted(long long B, int N, const double* m, const double* s, const double* acc,
+                                   const float* acc32, double shift, double* pk, hipStream_t st) {
+  long long blocks = (B * (2LL * N + 2) + 255) / 256;
+  blocks = blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks);
+  hipLaunchKernelGGL(k_pack_shifted, dim3((unsigned)blocks), dim3(256), 0, st, B, N, m, s, acc, acc32, shift, pk);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -490,7 +532,8 @@ hipError_t qce_launch_pack_f64all(int K, int M, int N, int MP, int NP, int has_m
 template <int MP, int NP, bool HM, bool OP>
 static hipError_t launch_f64_t(const QceF64Args& a, hipStream_t st) {
   hipLaunchKernelGGL((k_est_all_f64<MP, NP, HM, F64_CT, F64_NW, OP>), dim3((unsigned)a.nwg), dim3(F64_NW * 64), 0, st,
-                     a.B, a.M, a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa);
+                     a.B, a.M, a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa,
+                     a.pk, a.shift);
   return hipGetLastError();
 }
 
@@ -515,7 +558,8 @@ hipError_t qce_launch_est_f64(const QceF64Args& a, bool out_partial, hipStream_t
     const long long nb = a.B - b0;
     hipLaunchKernelGGL(k_merge_f64, dim3((unsigned)((nb + 3) / 4)), dim3(256), 0, st, nb, a.N, a.K, F64_TS, a.L,
                        a.pm, a.ps, a.pa, out_partial ? nullptr : a.h + b0 * a.N, a.om ? a.om + b0 : nullptr,
-                       a.os ? a.os + b0 : nullptr, a.oa ? a.oa + b0 * 2 * a.N : nullptr);
+                       a.os ? a.os + b0 : nullptr, a.oa ? a.oa + b0 * 2 * a.N : nullptr,
+                       a.pk ? a.pk + b0 * (2 * a.N + 2) : nullptr, a.shift);
     e = hipGetLastError();
   }
   return e;

@@ -94,6 +94,8 @@ struct QceF64Args {
   double2* h;           // final output (or nullptr with out_partial)
   double *om, *os, *oa;  // partial-format output (K-shard path), oa B x 2N
   double *pm, *ps, *pa;  // scratch for cut tiles: nwg * 2 * tile records
+  double* pk = nullptr;   // shifted packed partial B x (2N+2): [s e^{m-shift}, 0, acc e^{m-shift}] (instead of om/os/oa)
+  double shift = 0.0;
 };
 bool qce_f64_shape(int MP, int NP);
 int qce_f64_tile();
@@ -102,6 +104,8 @@ hipError_t qce_launch_pack_f64all(int K, int M, int N, int MP, int NP, int has_m
                                   const double2* W, const double2* q0, const double2* bvec, double* pack,
                                   hipStream_t st);
 hipError_t qce_launch_est_f64(const QceF64Args& a, bool out_partial, hipStream_t st);
+hipError_t qce_launch_pack_shifted(long long B, int N, const double* m, const double* s, const double* acc,
+                                   const float* acc32, double shift, double* pk, hipStream_t st);
 hipError_t qce_launch_f64_to_f32(const double* a, float* b, long long n, hipStream_t st);
 hipError_t qce_launch_f32_to_f64(const float* a, double* b, long long n, hipStream_t st);
 

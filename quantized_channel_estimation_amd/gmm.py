@@ -25,6 +25,56 @@ except Exception:  # pragma: no cover - sklearn is part of the image
     _SkGaussianMixture = None
 
 
+_MIRRORED = ("means_", "covariances_", "precisions_cholesky_")
+
+
+def _materialize(gm):
+    """Fetch the observation-domain state a previous estimate left pending (see _mirror)."""
+    pend = gm.__dict__.pop("_qce_pending", None)
+    if pend is not None:
+        pend(gm)
+
+
+if _SkGaussianMixture is not None:
+    class _GaussianMixtureState(_SkGaussianMixture):
+        """sklearn's GaussianMixture parameter bag (the reference keeps its fitted state in one,
+        gmm_cplx_bussgang.py:86-87) whose observation-domain attributes ``means_``, ``covariances_``
+        and ``precisions_cholesky_`` — rewritten by every estimate (:262-264, :288, :309-313) — are
+        copied from the device only when first read: an estimate does not pay for ~50 MB of table
+        transfers that the scripts never look at."""
+
+        def __getattr__(self, name):
+            if name in _MIRRORED and "_qce_pending" in self.__dict__:
+                _materialize(self)
+                return self.__dict__[name]
+            raise AttributeError(name)
+
+        def __getstate__(self):
+            _materialize(self)
+            return super().__getstate__()
+else:  # pragma: no cover
+    _GaussianMixtureState = None
+
+
+def _fingerprint(*arrays):
+    """Content key of the model parameters (in-place edits of means_cplx / covs_cplx / weights_
+    invalidate the device model, as the reference re-reads them on every estimate_from_y)."""
+    try:
+        import xxhash
+        hs = xxhash.xxh3_64()
+    except Exception:  # pragma: no cover
+        import hashlib
+        hs = hashlib.blake2b(digest_size=8)
+    for a in arrays:
+        if a is None:
+            hs.update(b"none")
+            continue
+        a = np.ascontiguousarray(a)
+        hs.update(str((a.shape, a.dtype.str)).encode())
+        hs.update(a.view(np.uint8).reshape(-1))
+    return hs.hexdigest()
+
+
 class _ParamBag:
     """Minimal stand-in for sklearn's GaussianMixture when sklearn is not importable."""
 
@@ -69,7 +119,7 @@ class Gmm_nbit:
 
     def __init__(self, *gmm_args, device=0, precision="f64", **gmm_kwargs):
         if _SkGaussianMixture is not None:
-            self.gm = _SkGaussianMixture(*gmm_args, **gmm_kwargs)
+            self.gm = _GaussianMixtureState(*gmm_args, **gmm_kwargs)
         else:
             self.gm = _ParamBag(*gmm_args, **gmm_kwargs)
         self.means_cplx = None
@@ -96,6 +146,8 @@ class Gmm_nbit:
         obj = cls.__new__(cls)
         Gmm_nbit.__init__(obj, device=device)
         obj.gm = copy.deepcopy(ref.gm)
+        if _GaussianMixtureState is not None and type(obj.gm) is _SkGaussianMixture:
+            obj.gm.__class__ = _GaussianMixtureState
         for name in ("means_cplx", "covs_cplx", "fft_covs", "fft_means", "chol", "F2"):
             setattr(obj, name, copy.deepcopy(getattr(ref, name, None)))
         obj.params = copy.deepcopy(getattr(ref, "params", {}))
@@ -193,6 +245,8 @@ class Gmm_nbit:
 
     # ------------------------------------------------------------------ pickling (pool.starmap, :282-287)
     def __getstate__(self):
+        if hasattr(self.gm, "__dict__"):
+            _materialize(self.gm)
         d = self.__dict__.copy()
         d["_dev"] = None
         d["_dev_key"] = None
@@ -222,7 +276,7 @@ class Gmm_nbit:
         means = self.means_cplx
         w = np.asarray(self.gm.weights_, dtype=float)
         precision = getattr(self, "precision", "f64")
-        key = (id(self.covs_cplx), id(means), id(self.gm.weights_), covs.shape, self.device, precision)
+        key = (_fingerprint(covs, means, w), self.device, precision)
         if self._dev is None or self._dev_key != key:
             self._dev = _lib.DeviceModel(means, covs, w, device=self.device)
             if precision != "f64":
@@ -235,11 +289,18 @@ class Gmm_nbit:
         """Reproduce the reference's mutation of ``self.gm`` (:262-264, :288, :309-313)."""
         if not self.mirror_state:
             return
-        t = dev.tables()
-        self.gm.means_ = t["means_y"]
-        self.gm.covariances_ = t["Cr"]
-        self.gm.precisions_cholesky_ = t["P"]
         self.gm.n_features_in_ = M
+
+        def fetch(gm, dev=dev):
+            t = dev.tables(("means_y", "Cr", "P"))
+            gm.__dict__.update(means_=t["means_y"], covariances_=t["Cr"], precisions_cholesky_=t["P"])
+
+        if _GaussianMixtureState is not None and isinstance(self.gm, _GaussianMixtureState):
+            for n in _MIRRORED:
+                self.gm.__dict__.pop(n, None)
+            self.gm.__dict__["_qce_pending"] = fetch  # read lazily (_GaussianMixtureState.__getattr__)
+        else:
+            fetch(self.gm)
 
     def _prepare(self, A, snr_dB, n_bits, quantizer_type, quantizer, allow_inf=True):
         dev = self._device_model()

@@ -1,17 +1,23 @@
-"""Multi-GPU decomposition of the estimate path (one process per GPU, torch.distributed).
+"""Multi-GPU decomposition of the estimate path (one process per GPU, torch.distributed over RCCL).
 
-Two ways to split one SNR point's work:
+The reference's only parallelism is a process pool over SNR points (Bussgang_GMM.py:29-32, :287);
+here one SNR point's batch is split over the GPUs of a node, two ways:
 
+* **component shards** (``ComponentShardEstimator``, the north-star split): rank g holds the
+  components K_g.  The shift M* = max_k c_k over ALL components (c_k = log w_k + 2 log det P_k
+  - M log pi >= lp_bk because the quad form is >= 0; one scalar MAX all-reduce per SNR) is common
+  to every shard, so each rank's partial can be written already scaled,
+  row b = [s_b e^{m_b - M*}, 0, acc_b e^{m_b - M*}] (``qce_estimate_partial_shifted``, FP64), and ONE
+  SUM collective of these (B, 2N+2) rows gives h_b = acc / s.  The batch is cut into chunks; chunk
+  i's collective (reduce-scatter by default: each rank keeps its slice of the rows, half the bytes
+  of an all-reduce) is issued asynchronously and runs on RCCL's stream while chunk i+1's partial
+  kernel runs on the compute stream.  Rows whose sum underflows everywhere (min quad form > ~700
+  above M*) are detected with one small all-reduce per step and recombined exactly (MAX of m, then
+  SUM).
 * **batch shards** (``BatchShardEstimator``): every rank holds the whole mixture and estimates a
-  disjoint slice of the observations.  No data-path collective — the samples are independent.
-* **component shards** (``ComponentShardEstimator``): rank g holds components K_g and returns, per
-  sample, the running max m_g, s_g = sum_{k in K_g} e^{lp_k - m_g} and
-  acc_g = sum_{k in K_g} e^{lp_k - m_g} (W_k y + b_k) (``qce_estimate_partial``).  With the
-  y-independent shift M* = max_k c_k >= lp_k (c_k = log w_k + 2 log det P_k - M log pi, known after
-  prepare; one scalar MAX all-reduce per SNR) every rank rescales to s'_g = s_g e^{m_g - M*},
-  acc'_g = acc_g e^{m_g - M*} in FP64 and ONE SUM all-reduce of the packed (B, 2N+1) buffer gives
-  h = acc / s.  Rows whose s underflows everywhere (all quad forms > ~700) are recombined with a
-  MAX all-reduce of m first.
+  disjoint slice of the observations.  No data-path collective — the samples are independent (the
+  configuration for the HBM-bound Fourier paths, where a K-shard collective costs more than the
+  kernel).
 """
 import numpy as np
 
@@ -32,6 +38,13 @@ def combine_partials_numpy(parts, N):
     return acc[:, 0::2] + 1j * acc[:, 1::2]
 
 
+def combine_packed_numpy(packed_parts):
+    """Host combine of shifted packed partials [(B, 2N+2), ...] (same shift) -> h (B, N)."""
+    tot = np.sum([np.asarray(p, dtype=np.float64) for p in packed_parts], axis=0)
+    acc = tot[:, 2:] / tot[:, :1]
+    return acc[:, 0::2] + 1j * acc[:, 1::2]
+
+
 def component_slices(K, world):
     """Contiguous, balanced component ranges per rank."""
     base, rem = divmod(K, world)
@@ -48,10 +61,10 @@ def batch_slices(B, world):
 
 
 def combine_partials_dist(m, s, acc, shift, N, group=None):
-    """Distributed combine of one rank's partial (torch tensors on this rank's device).
-
-    m, s: (B,) float64; acc: (B, 2N) float32; shift: the global M* (python float).
-    Returns h (B, N) complex128 on every rank.  One SUM all-reduce on the data path."""
+    """Exact distributed combine of one rank's unshifted partial (torch tensors on this rank's device):
+    m, s (B,) float64, acc (B, 2N) float32/float64, shift = the global M*.  One SUM all-reduce of the
+    rescaled rows; rows that underflow under M* take the MAX-then-SUM path.  h (B, N) complex128 on every
+    rank.  (The pipelined path of ComponentShardEstimator uses this only as its underflow fallback.)"""
     import torch
     import torch.distributed as dist
     B = m.shape[0]
@@ -65,7 +78,7 @@ def combine_partials_dist(m, s, acc, shift, N, group=None):
     dist.all_reduce(nbad, op=dist.ReduceOp.MAX, group=group)  # tiny: agree on the fallback
     if int(nbad.item()) > 0:
         idx = torch.nonzero(bad, as_tuple=False).flatten()
-        # underflow guard: exact two-step combine for the affected rows
+        # underflow guard: exact two-step combine for the affected rows (every rank has the same rows)
         mm = m[idx].clone()
         dist.all_reduce(mm, op=dist.ReduceOp.MAX, group=group)
         sc2 = torch.exp(m[idx] - mm)
@@ -78,39 +91,136 @@ def combine_partials_dist(m, s, acc, shift, N, group=None):
     return torch.complex(out[:, 0::2].contiguous(), out[:, 1::2].contiguous())
 
 
+def chunk_bounds(B, chunks, world, scatter):
+    """Row ranges of the pipeline chunks; with scatter every chunk but the last has a multiple of
+    `world` rows and the last one is padded up to one (reduce_scatter splits rows evenly)."""
+    chunks = max(1, min(int(chunks), max(1, B // max(world, 1))))
+    step = -(-B // chunks)
+    if scatter:
+        step = -(-step // world) * world
+    out, lo = [], 0
+    while lo < B:
+        hi = min(B, lo + step)
+        out.append((lo, hi))
+        lo = hi
+    return out
+
+
+def _packed_to_complex(rows):
+    import torch
+    acc = rows[:, 2:] / rows[:, :1]
+    return torch.complex(acc[:, 0::2].contiguous(), acc[:, 1::2].contiguous())
+
+
 class ComponentShardEstimator:
     """K-sharded 'all'-mode estimator: this rank's slice of the mixture on its own GPU."""
 
-    def __init__(self, means_cplx, covs_cplx, weights, rank, world, device=0, group=None):
+    def __init__(self, means_cplx, covs_cplx, weights, rank, world, device=0, group=None, precision="f64"):
         K = np.asarray(covs_cplx).shape[0]
+        self.rank, self.world = rank, world
         self.lo, self.hi = component_slices(K, world)[rank]
         sl = slice(self.lo, self.hi)
         means = None if means_cplx is None else np.asarray(means_cplx)[sl]
         self.dev = _lib.DeviceModel(means, np.asarray(covs_cplx)[sl], np.asarray(weights)[sl], device=device)
+        if precision != "f64":
+            self.dev.set_precision(precision)
         self.N = self.dev.N
         self.group = group
         self.shift = None
+        self._bufs = {}
 
     def prepare(self, A, snr_db, n_bits, quant_kind=_lib.QUANT_UNIFORM, thresholds=None, labels=None, stream=None):
+        """Per-rank prepare of its components and the common shift M* (one scalar MAX all-reduce)."""
         import torch
         import torch.distributed as dist
         self.dev.prepare(A, snr_db, n_bits, quant_kind, thresholds, labels, stream=stream)
-        c = self.dev.tables()["cconst"]
+        c = self.dev.cconst()
         dev = torch.device("cuda", self.dev.device) if torch.cuda.is_available() else torch.device("cpu")
         t = torch.tensor([float(np.max(c))], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         self.shift = float(t.item())
 
-    def estimate(self, y, stream=None):
-        m, s, acc = self.dev.partial(y, stream=stream)
-        return combine_partials_dist(m, s, acc, self.shift, self.N, self.group)
+    def _buf(self, key, shape, device):
+        import torch
+        b = self._bufs.get(key)
+        if b is None or tuple(b.shape) != tuple(shape):
+            b = torch.empty(shape, dtype=torch.float64, device=device)
+            self._bufs[key] = b
+        return b
+
+    def estimate(self, y, chunks=4, scatter=True):
+        """'all'-mode estimates of y (B, M) complex128 CUDA tensor.
+
+        scatter=True: reduce-scatter per chunk, returns (rows, h) with h (n, N) complex128 the estimates of
+        this rank's rows (global row indices `rows`, a LongTensor); scatter=False: all-reduce, every rank
+        gets h for all B rows (rows = None).  The partial kernels run on torch's current stream, each
+        chunk's collective asynchronously on RCCL's stream behind it."""
+        import torch
+        import torch.distributed as dist
+        B = y.shape[0]
+        W = 2 * self.N + 2
+        dev = y.device
+        stream = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else None
+        multi = self.world > 1
+        use_rs = scatter and multi
+        bounds = chunk_bounds(B, chunks, self.world, use_rs)
+        works, pieces = [], []
+        for i, (lo, hi) in enumerate(bounds):
+            n = hi - lo
+            npad = -(-n // self.world) * self.world if use_rs else n
+            pk = self._buf(("pk", i), (npad, W), dev)
+            if npad > n:
+                pk[n:].zero_()
+            self.dev.partial_shifted(y[lo:hi], self.shift, out=pk[:n], stream=stream)
+            if use_rs:
+                out = self._buf(("rs", i), (npad // self.world, W), dev)
+                works.append(dist.reduce_scatter_tensor(out, pk, op=dist.ReduceOp.SUM, group=self.group,
+                                                        async_op=True))
+                r0 = lo + self.rank * (npad // self.world)
+                pieces.append((r0, min(hi, r0 + npad // self.world), out))
+            else:
+                if multi:
+                    works.append(dist.all_reduce(pk[:n], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+                pieces.append((lo, hi, pk[:n]))
+        for wk in works:
+            wk.wait()
+        rows = torch.cat([r[:max(0, b - a)] for a, b, r in pieces]) if pieces else None
+        # underflow guard: one tiny collective per step agrees on whether any row summed to s = 0
+        nbad = (rows[:, 0] == 0).sum().to(torch.float64).reshape(1)
+        if multi:
+            dist.all_reduce(nbad, op=dist.ReduceOp.MAX, group=self.group)
+        if float(nbad.item()) > 0:
+            return self._exact(y, use_rs, pieces)
+        h = _packed_to_complex(rows)
+        if not use_rs:
+            return None, h
+        idx = torch.cat([torch.arange(a, max(a, b), device=dev) for a, b, _ in pieces])
+        return idx, h
+
+    def _exact(self, y, use_rs, pieces):
+        """Rare path: exact two-step combine of the unshifted FP64 partials for the whole batch."""
+        import torch
+        stream = torch.cuda.current_stream(y.device).cuda_stream if y.device.type == "cuda" else None
+        m, s, acc = self.dev.partial64(y, stream=stream)
+        if self.world > 1:
+            h = combine_partials_dist(m, s, acc, self.shift, self.N, self.group)
+        else:
+            h = torch.from_numpy(combine_partials_numpy([(m.cpu().numpy(), s.cpu().numpy(), acc.cpu().numpy())],
+                                                        self.N)).to(y.device)
+        if not use_rs:
+            return None, h
+        idx = torch.cat([torch.arange(a, max(a, b), device=y.device) for a, b, _ in pieces])
+        return idx, h[idx]
 
 
 class BatchShardEstimator:
     """Batch-sharded replicas: the full mixture on every GPU, a disjoint slice of y per rank."""
 
-    def __init__(self, means_cplx, covs_cplx, weights, device=0):
+    def __init__(self, means_cplx, covs_cplx, weights, device=0, precision="f64"):
         self.dev = _lib.DeviceModel(means_cplx, covs_cplx, weights, device=device)
+        if precision != "f64":
+            self.dev.set_precision(precision)
 
     def prepare(self, *args, **kw):
         self.dev.prepare(*args, **kw)
