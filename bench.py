@@ -211,7 +211,7 @@ def cpu_baseline(cfg, means, covs, w, y, quantizer, budget_s):
 def f64_executed_flops(N, K, B):
     """Executed v_mfma_f64_16x16x4 work of k_est_all_f64: 256 flops per sample per 1 KB table block
     (GL: NTL(NTL+1) blocks — Linv's upper triangle skipped; GW: NTW*KP blocks)."""
-    Np = 16 if N <= 16 else (32 if N <= 32 else 64)
+    Np = 16 if N <= 16 else (32 if N <= 32 else (64 if N <= 64 else 128))
     ntl, ntw, kp = Np // 8, Np // 8, Np // 4
     return 256.0 * (ntl * (ntl + 1) + ntw * kp) * K * B
 
@@ -232,7 +232,7 @@ def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
                     fp64_flops_per_launch=fft_flops, fp64_tflops=round(fft_flops / (kern_ms * 1e-3) / 1e12, 3))
     flops = 16.0 * k_local * N * N * B  # 16 K M N real flops per estimate
     achieved = flops / (kern_ms * 1e-3) / 1e12
-    if dm.precision == "f64" and N <= 64:
+    if dm.precision == "f64" and N <= 128:
         ex = f64_executed_flops(N, k_local, B)
         return dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
                     frac=round(achieved / FP64_MFMA_PEAK_TFLOPS, 4), traffic=traffic,
@@ -240,8 +240,8 @@ def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
                     kernel_ms=round(kern_ms, 4), flops_per_launch=flops, executed_flops_per_launch=ex,
                     mfma_issue_frac=round(ex / (kern_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
                     note="algorithmic flops (16KMN) / time; frac can exceed 1 because the upper triangle of "
-                         "Linv is skipped (executed = 0.78 of algorithmic at N=64): mfma_issue_frac is the "
-                         "executed-MFMA fraction of the FP64 peak")
+                         "Linv is skipped (executed = %.3f of algorithmic here): mfma_issue_frac is the "
+                         "executed-MFMA fraction of the FP64 peak" % (ex / flops))
     nsl = (2 * N) // 32
     tri = (sum(2 * r + 2 for r in range(nsl)) / (nsl * 2 * nsl) + 1.0) / 2.0
     ex = flops * tri * 2.0
@@ -255,7 +255,7 @@ def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
 def dtype_of(dm):
     if dm.structure()[2]:
         return "f64"
-    if dm.precision == "f64" and dm.N <= 64:
+    if dm.precision == "f64" and dm.N <= 128:
         return "f64"
     return "f16x2 (fp16 hi+lo split, fp32 accumulate, fp64 softmax)"
 

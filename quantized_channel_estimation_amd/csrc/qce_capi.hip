@@ -188,7 +188,7 @@ bool want_f64(const qce_model* m) {
 // (m, s, acc) partial when h == nullptr (K-shard path)
 int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, double* oa,
             hipStream_t st, double* pk = nullptr, double shift = 0.0) {
-  const long long TS = qce_f64_tile();
+  const long long TS = qce_f64_tile(m->MP, m->NP);
   const long long tiles = (B + TS - 1) / TS;
   long long slots = m->cu_count;  // 128 KB of LDS: one workgroup per CU
   const char* e = getenv("QCE_WORKGROUPS");

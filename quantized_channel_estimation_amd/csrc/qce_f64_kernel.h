@@ -1,0 +1,424 @@
+// Fused 'all'-mode estimate kernel in FP64 on v_mfma_f64_16x16x4_f64 (gfx950 / CDNA4) — the
+// reference-precision path of estimate_from_y (gmm_cplx_bussgang.py:220-228 with :331-332,
+// :388-435, :632-656; every reference step is complex128).
+//
+//   lp_bk = c_k - || E(Linv_k) [y_b; 1] ||^2          (the -q0 column folds the mean in)
+//   h_b   = sum_k e^{lp_bk - m_b} E(W_k) [y_b; 1] / sum_k e^{lp_bk - m_b}
+//
+// E(.) is the real 2x2-block embedding of a complex matrix; every product is an FP64 MFMA with
+// FP64 accumulation, the softmax is FP64 (libm exp), so the result is an FP64 computation of the
+// reference's formula (only the summation order differs).
+//
+// Layout (prepare: k_pack_f64all).  The k (reduction) order is permuted so that one 16-byte load
+// of y gives a lane both B-operand values of a "k-pair": k-step 2s+e, lane group g = lane>>4
+// holds part e of complex column 4s+g.  Output rows are permuted so that a lane's four
+// accumulator registers are (re, im) of complex rows 8T+g and 8T+4+g: row rho of row tile T is
+// complex 8T + 4(rho>>3) + (rho&3), part (rho>>2)&1.  A table "block" is 1 KB: the A operands of
+// one row tile for the two k-steps of a k-pair, lane-major (lane l: 16 B = both k-steps), read
+// with one conflict-free ds_read_b128.
+//   component k: GL blocks (row tile T outer; k-pairs 0..2T+1 — the upper triangle of Linv is
+//   skipped; + one mean block with the -q0 column), then GW blocks (k-pair outer, row tile inner,
+//   + one mean block per row tile with the b column), padded to whole ring chunks.
+//
+// Scheduling: one workgroup = NW waves x 16*CT samples (CT column tiles per wave; samples on the
+// MFMA column axis, so quad form, running max, sum and weights are per-lane registers and the
+// y fragments stay in VGPRs for the whole component loop).  The component tables stream through
+// an LDS ring of NSLOT chunks of 16 KB (global_load_lds, 16 B per lane); one barrier per chunk,
+// executed E blocks before the chunk is needed so the LDS reads of its first blocks are not held
+// up.  Persistent grid: R rounds of whole tiles per workgroup, then the remaining tiles' (tile,
+// component) items dealt out L per workgroup (stream-K); a tile cut between workgroups leaves
+// FP64 partials (m, s, acc) that k_merge_f64 combines — the same format as the K-shard path.
+#pragma once
+#include "qce_common.h"
+#include "qce_kernels.h"
+#include "qce_h2_common.h"
+
+#include <utility>
+
+namespace {
+
+template <int MP, int NP, bool HM>
+struct F64G {
+  static constexpr int NTL = MP / 8;  // GL row tiles (16 real rows = 8 complex rows)
+  static constexpr int NTW = NP / 8;  // GW row tiles
+  static constexpr int KP = MP / 4;   // k-pairs (4 complex columns)
+  static constexpr int HMI = HM ? 1 : 0;
+  static constexpr int GL_BLOCKS = NTL * (NTL + 1) + HMI * NTL;
+  static constexpr int GW_BLOCKS = NTW * (KP + HMI);
+  static constexpr int BLOCKS = GL_BLOCKS + GW_BLOCKS;
+  static constexpr int CB = 16;  // blocks per ring chunk (16 KB)
+  static constexpr int BPC = (BLOCKS + CB - 1) / CB * CB;
+  static constexpr int CPC = BPC / CB;
+  static constexpr __host__ __device__ int gl_off(int T) { return T * (T + 1) + HMI * T; }
+};
+
+constexpr int F64_NSLOT = 8;                // ring slots (128 KB of LDS)
+constexpr int F64_CHUNK = 16 * 1024;
+
+// block b of a component -> kind (0 GL data, 1 GL mean, 2 GW data, 3 GW mean, 4 pad), tile T, k-pair s
+struct BlockInfo {
+  int kind, T, s;
+};
+template <int MP, int NP, bool HM>
+constexpr BlockInfo block_info(int b) {
+  using G = F64G<MP, NP, HM>;
+  if (b < G::GL_BLOCKS) {
+    int T = 0;
+    while (b >= G::gl_off(T + 1)) ++T;
+    const int s = b - G::gl_off(T);
+    return BlockInfo{s < 2 * T + 2 ? 0 : 1, T, s};
+  }
+  const int r = b - G::GL_BLOCKS;
+  if (r < G::KP * G::NTW) return BlockInfo{2, r % G::NTW, r / G::NTW};
+  if (r < (G::KP + G::HMI) * G::NTW) return BlockInfo{3, r - G::KP * G::NTW, G::KP};
+  return BlockInfo{4, 0, 0};
+}
+
+template <int N_>
+QCE_DEV void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N_) : "memory");
+}
+
+QCE_DEV double sum_groups(double q) {  // sum over the four 16-lane groups (all lanes get the total)
+  q += __shfl_xor(q, 16);
+  q += __shfl_xor(q, 32);
+  return q;
+}
+
+// Source cursor of the ring: which component chunk a workgroup streams next.  Items are the
+// workgroup's (tile, component) work in order: R*K full-round items (components 0..K-1 per tile),
+// then the tail items item0 .. item0+ntail-1 (component = item % K).
+struct RingCursor {
+  int item, nitems, rk, comp_tail, comp, cc, K, cpc;
+  QCE_DEV void init(int rk_, int comp_tail_, int ntail, int K_, int cpc_) {
+    rk = rk_;
+    comp_tail = comp_tail_;
+    nitems = rk_ + ntail;
+    K = K_;
+    cpc = cpc_;
+    item = 0;
+    cc = 0;
+    comp = rk_ > 0 ? 0 : comp_tail_;
+  }
+  QCE_DEV long long chunk_index() const { return (long long)(comp * cpc + cc); }
+  QCE_DEV void advance() {
+    if (item >= nitems) return;
+    if (++cc < cpc) return;
+    cc = 0;
+    ++item;
+    if (item >= nitems) {  // past the end: keep re-loading the last chunk (dummy, never read)
+      item = nitems;
+      cc = cpc - 1;
+      return;
+    }
+    if (item == rk) comp = comp_tail;
+    else comp = (comp + 1 == K) ? 0 : comp + 1;
+  }
+};
+
+// one chunk = 16 wave-instructions of 1 KB, LPW per wave (wave-uniform addresses, no branches)
+template <int NW>
+QCE_DEV void issue_chunk(const char* __restrict__ src, char* dst, int wave, int lane) {
+  constexpr int LPW = (F64_CHUNK / 1024) / NW;
+  src += wave * 1024 + lane * 16;
+  dst += wave * 1024;
+#pragma unroll
+  for (int i = 0; i < LPW; ++i)
+    __builtin_amdgcn_global_load_lds((const void*)(src + i * NW * 1024),
+                                     (__attribute__((address_space(3))) void*)(dst + i * NW * 1024), 16, 0, 0);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// fused kernel
+// ---------------------------------------------------------------------------
+template <int MP, int NP, bool HM, int CT, int NW, bool OUT_PARTIAL>
+__global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int N, int K, int R, long long L,
+                                                         const double2* __restrict__ y, const char* __restrict__ pack,
+                                                         const double* __restrict__ cconst, double2* __restrict__ h,
+                                                         double* __restrict__ om, double* __restrict__ os,
+                                                         double* __restrict__ oa, double* __restrict__ pm,
+                                                         double* __restrict__ ps, double* __restrict__ pa,
+                                                         double* __restrict__ pk, double shift) {
+  using G = F64G<MP, NP, HM>;
+  constexpr int TS = NW * 16 * CT;           // samples per tile
+  constexpr int LPW = (F64_CHUNK / 1024) / NW;  // global_load_lds per wave per chunk
+  constexpr int E = 2;                        // boundary lead (blocks) = LDS prefetch distance
+  constexpr double RESCALE = 32.0;            // lazy max: rescale only when lp exceeds m by this
+  static_assert((F64_CHUNK / 1024) % NW == 0, "chunk split");
+  __shared__ __attribute__((aligned(16))) char lds[F64_NSLOT * F64_CHUNK];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g = lane >> 4, col = lane & 15;
+  const long long P = gridDim.x, w = blockIdx.x;
+  const long long tiles = (B + TS - 1) / TS;
+  const long long tail0 = (long long)R * P;
+  const long long item0 = w * L;
+  const long long tail_items = (tiles - tail0) * K;
+  const long long item1 = (item0 + L < tail_items) ? item0 + L : tail_items;
+  const long long ntail = item1 > item0 ? item1 - item0 : 0;
+  if ((long long)R == 0 && ntail == 0) return;  // nothing for this workgroup (uniform)
+  const long long t_first = tail0 + (L > 0 ? item0 / K : 0);
+  const long long nseg = (long long)R + (ntail > 0 ? (item1 - 1) / K - item0 / K + 1 : 0);
+
+  // ---- ring ----
+  RingCursor cur;
+  cur.init(R * K, (int)(item0 % K), (int)ntail, K, G::CPC);
+  int issued = 0;  // chunks issued so far (stream index of the next one)
+  auto issue_next = [&]() {
+    const char* src = pack + cur.chunk_index() * (long long)F64_CHUNK;
+    char* dst = lds + (issued & (F64_NSLOT - 1)) * F64_CHUNK;
+    issue_chunk<NW>(src, dst, wave, lane);
+    cur.advance();
+    ++issued;
+  };
+  // boundary for stream chunk jn: its loads landed everywhere, and every wave is done with chunk
+  // jn - 2, whose slot is refilled with chunk jn + NSLOT - 2
+  auto boundary = [&]() {
+    wait_vmcnt<(F64_NSLOT - 3) * LPW>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    issue_next();
+  };
+#pragma unroll 1
+  for (int j = 0; j < F64_NSLOT - 2; ++j) issue_next();
+  boundary();  // chunk 0
+  int cstream = 0;  // stream index of the current component's chunk 0
+
+  for (long long seg = 0; seg < nseg; ++seg) {
+    long long t;
+    int klo, khi;
+    if (seg < R) {
+      t = seg * P + w;
+      klo = 0;
+      khi = K;
+    } else {
+      t = tail0 + item0 / K + (seg - R);
+      const long long tK = (t - tail0) * K;
+      klo = (int)((item0 > tK ? item0 : tK) - tK);
+      khi = (int)((tK + K < item1 ? tK + K : item1) - tK);
+    }
+    const long long sbase = t * TS + (long long)wave * 16 * CT;
+    // y fragments: k-pair s, lane group g -> complex column 4s + g (re: k-step 2s, im: 2s+1)
+    // y fragments: k-pair s, lane group g -> complex column 4s + g (re: k-step 2s, im: 2s+1).  Rows past B
+    // and columns past M are clamped (finite values of the same tensor) instead of masked: a padded column
+    // meets zero table entries, an invalid sample is never written.  The laundered lane constants keep the
+    // per-column offsets inside the loop (hoisted, they would pin a register each for the whole kernel).
+    double2 yv[CT][G::KP];
+    int gl = g, cl = col;
+    asm volatile("" : "+v"(gl), "+v"(cl));
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      long long sm = sbase + 16 * c + cl;
+      sm = sm < B ? sm : B - 1;
+      const double2* yr = y + sm * M;
+#pragma unroll
+      for (int s = 0; s < G::KP; ++s) {
+        const int cc = 4 * s + gl;
+        yv[c][s] = yr[cc < M ? cc : M - 1];
+      }
+    }
+    wait_vmcnt<0>();
+    f64x4 out[G::NTW][CT];
+#pragma unroll
+    for (int T = 0; T < G::NTW; ++T)
+#pragma unroll
+      for (int c = 0; c < CT; ++c) out[T][c] = f64x4{0.0, 0.0, 0.0, 0.0};
+    double m[CT], ssum[CT];
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      m[c] = QCE_NEG_INF;
+      ssum[c] = 0.0;
+    }
+
+#pragma unroll 1
+    for (int k = klo; k < khi; ++k) {
+      const double ck = cconst[k];
+      const int slot0 = cstream & (F64_NSLOT - 1);
+      // LDS offset of this lane's 16 B in the slot of the chunk being read; advanced when the reads cross
+      // into the next chunk and laundered, so the compiler keeps one live offset instead of hoisting one
+      // per chunk of the unrolled component
+      int rslot = slot0;
+      int roff = lane * 16 + rslot * F64_CHUNK;
+      auto rd = [&](int off) -> double2 { return *reinterpret_cast<const double2*>(&lds[roff + off]); };
+      f64x4 acc[CT];
+      double qp[CT], p[CT];
+      double bs0[CT], bs1[CT];
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        qp[c] = 0.0;
+        p[c] = 0.0;
+        bs0[c] = bs1[c] = 0.0;
+        acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
+      }
+      double2 buf[E + 1];
+#pragma unroll
+      for (int i = 0; i < E; ++i) buf[i] = rd(i * 1024);
+      static_for(
+          [&](auto bc) {
+            constexpr int b = decltype(bc)::value;
+            constexpr BlockInfo bi = block_info<MP, NP, HM>(b);
+            __builtin_amdgcn_sched_barrier(0);  // keep the explicit prefetch distance (no LDS read hoisting)
+            // next chunk's boundary E blocks early (the last one is the next component's chunk 0)
+            if constexpr ((b + E) % G::CB == 0) boundary();
+            if constexpr (b + E < G::BPC) {
+              constexpr int r = b + E;
+              if constexpr (r % G::CB == 0) {
+                rslot = (rslot + 1) & (F64_NSLOT - 1);
+                roff = lane * 16 + rslot * F64_CHUNK;
+                asm volatile("" : "+v"(roff));
+              }
+              buf[r % (E + 1)] = rd((r % G::CB) * 1024);
+            }
+            const double2 a = buf[b % (E + 1)];
+            if constexpr (bi.kind == 0) {  // GL data: u += E(Linv) y over k-pair s
+#pragma unroll
+              for (int c = 0; c < CT; ++c) acc[c] = mfma16x16x4d(a.x, yv[c][bi.s].x, acc[c]);
+#pragma unroll
+              for (int c = 0; c < CT; ++c) acc[c] = mfma16x16x4d(a.y, yv[c][bi.s].y, acc[c]);
+            } else if constexpr (bi.kind == 1) {  // GL mean column (-q0): B = 1 in lane group 0
+              const double one = g == 0 ? 1.0 : 0.0;
+#pragma unroll
+              for (int c = 0; c < CT; ++c) acc[c] = mfma16x16x4d(a.x, one, acc[c]);
+            } else if constexpr (bi.kind == 2) {  // GW data: out += E(W) (p y) over k-pair s
+              if constexpr (bi.T == 0) {
+#pragma unroll
+                for (int c = 0; c < CT; ++c) {
+                  bs0[c] = yv[c][bi.s].x * p[c];
+                  bs1[c] = yv[c][bi.s].y * p[c];
+                }
+              }
+#pragma unroll
+              for (int c = 0; c < CT; ++c) out[bi.T][c] = mfma16x16x4d(a.x, bs0[c], out[bi.T][c]);
+#pragma unroll
+              for (int c = 0; c < CT; ++c) out[bi.T][c] = mfma16x16x4d(a.y, bs1[c], out[bi.T][c]);
+            } else if constexpr (bi.kind == 3) {  // GW mean column (b): B = p in lane group 0
+#pragma unroll
+              for (int c = 0; c < CT; ++c) out[bi.T][c] = mfma16x16x4d(a.x, g == 0 ? p[c] : 0.0, out[bi.T][c]);
+            }
+            // end of a GL row tile: fold its squares into the quad form
+            if constexpr (bi.kind == 0 || bi.kind == 1) {
+              constexpr bool last = HM ? (bi.kind == 1) : (bi.s == 2 * bi.T + 1);
+              if constexpr (last) {
+#pragma unroll
+                for (int c = 0; c < CT; ++c) {
+                  qp[c] = fma(acc[c][0], acc[c][0], qp[c]);
+                  qp[c] = fma(acc[c][1], acc[c][1], qp[c]);
+                  qp[c] = fma(acc[c][2], acc[c][2], qp[c]);
+                  qp[c] = fma(acc[c][3], acc[c][3], qp[c]);
+                  // pin the fold here: sunk to the softmax, every row tile would keep its own accumulators
+                  asm volatile("" : "+v"(qp[c]));
+                  acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
+                }
+              }
+            }
+            // after the last GL block: log-probability and the online softmax (FP64)
+            if constexpr (b == G::GL_BLOCKS - 1) {
+              double lp[CT];
+              bool need = false;
+#pragma unroll
+              for (int c = 0; c < CT; ++c) {
+                lp[c] = ck - sum_groups(qp[c]);
+                need = need || (lp[c] > m[c] + RESCALE);
+              }
+              if (__builtin_amdgcn_ballot_w64(need) != 0ull) {  // rare: new running maximum
+#pragma unroll
+                for (int c = 0; c < CT; ++c) {
+                  const bool up = lp[c] > m[c] + RESCALE;
+                  const double mn = up ? lp[c] : m[c];
+                  const double al = up ? (m[c] == QCE_NEG_INF ? 0.0 : exp(m[c] - mn)) : 1.0;
+                  ssum[c] *= al;
+                  m[c] = mn;
+#pragma unroll
+                  for (int T = 0; T < G::NTW; ++T) out[T][c] *= al;
+                }
+              }
+#pragma unroll
+              for (int c = 0; c < CT; ++c) {
+                p[c] = (lp[c] == QCE_NEG_INF) ? 0.0 : exp(lp[c] - m[c]);
+                ssum[c] += p[c];
+              }
+            }
+          },
+          std::make_integer_sequence<int, G::BPC>{});
+      cstream += G::CPC;
+    }
+
+    // ---- write the tile ----
+    int gw = g;
+    asm volatile("" : "+v"(gw));
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const int ls = wave * 16 * CT + 16 * c + col;
+      const long long sample = t * TS + ls;
+      if (sample >= B) continue;
+      const bool whole = (klo == 0 && khi == K);
+      const bool pfmt = OUT_PARTIAL || !whole;
+      const long long row = whole ? sample : (w * 2 + (t == t_first ? 0 : 1)) * TS + ls;
+      if (OUT_PARTIAL && whole && pk) {  // shifted packed partial: [s e^{m-M*}, 0, acc e^{m-M*}] (K-shard sum)
+        const double sc = (m[c] == QCE_NEG_INF) ? 0.0 : exp(m[c] - shift);
+        double* dp = pk + sample * (2LL * N + 2);
+        if (g == 0) *reinterpret_cast<double2*>(dp) = make_double2(ssum[c] * sc, 0.0);
+#pragma unroll
+        for (int T = 0; T < G::NTW; ++T) {
+          const int i0 = 8 * T + gw, i1 = 8 * T + 4 + gw;
+          if (i0 < N) *reinterpret_cast<double2*>(dp + 2 + 2 * i0) = make_double2(out[T][c][0] * sc, out[T][c][1] * sc);
+          if (i1 < N) *reinterpret_cast<double2*>(dp + 2 + 2 * i1) = make_double2(out[T][c][2] * sc, out[T][c][3] * sc);
+        }
+      } else if (pfmt) {
+        double* dm = whole ? om : pm;
+        double* ds = whole ? os : ps;
+        double* da = (whole ? oa : pa) + row * (2LL * N);
+        if (g == 0) {
+          dm[row] = m[c];
+          ds[row] = ssum[c];
+        }
+#pragma unroll
+        for (int T = 0; T < G::NTW; ++T) {
+          const int i0 = 8 * T + gw, i1 = 8 * T + 4 + gw;
+          if (i0 < N) *reinterpret_cast<double2*>(da + 2 * i0) = make_double2(out[T][c][0], out[T][c][1]);
+          if (i1 < N) *reinterpret_cast<double2*>(da + 2 * i1) = make_double2(out[T][c][2], out[T][c][3]);
+        }
+      } else {
+        const double inv = 1.0 / ssum[c];
+        double2* hp = h + sample * N;
+#pragma unroll
+        for (int T = 0; T < G::NTW; ++T) {
+          const int i0 = 8 * T + gw, i1 = 8 * T + 4 + gw;
+          if (i0 < N) hp[i0] = make_double2(out[T][c][0] * inv, out[T][c][1] * inv);
+          if (i1 < N) hp[i1] = make_double2(out[T][c][2] * inv, out[T][c][3] * inv);
+        }
+      }
+    }
+  }
+  wait_vmcnt<0>();  // drain the (dummy) ring prefetches before the workgroup retires
+}
+
+// one launcher per padded observation dimension MP (instantiated in qce_f64_m<MP>.hip, compiled in
+// parallel): CT = 2 column tiles per wave when MP, NP <= 64, else 1 (a 128-dim observation's y fragments,
+// or a 128-row output accumulator, take the registers of two 64-dim ones)
+constexpr int qce_f64_ct(int MP, int NP) { return (MP <= 64 && NP <= 64) ? 2 : 1; }
+
+template <int MP, int NP, bool HM, bool OP>
+hipError_t qce_f64_launch_t(const QceF64Args& a, hipStream_t st) {
+  constexpr int CT = qce_f64_ct(MP, NP), NW = 4;
+  hipLaunchKernelGGL((k_est_all_f64<MP, NP, HM, CT, NW, OP>), dim3((unsigned)a.nwg), dim3(NW * 64), 0, st, a.B, a.M,
+                     a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa, a.pk, a.shift);
+  return hipGetLastError();
+}
+
+template <int MP>
+hipError_t qce_f64_launch_mp(const QceF64Args& a, bool out_partial, hipStream_t st) {
+  const bool hm = a.has_mean != 0;
+#define QCE_F64_NP(Y)                                                                                              \
+  if (a.NP == Y) {                                                                                                 \
+    if (out_partial) return hm ? qce_f64_launch_t<MP, Y, true, true>(a, st) : qce_f64_launch_t<MP, Y, false, true>(a, st); \
+    return hm ? qce_f64_launch_t<MP, Y, true, false>(a, st) : qce_f64_launch_t<MP, Y, false, false>(a, st);       \
+  }
+  QCE_F64_NP(16) QCE_F64_NP(32) QCE_F64_NP(64) QCE_F64_NP(128)
+#undef QCE_F64_NP
+  return hipErrorInvalidValue;
+}

@@ -98,7 +98,7 @@ struct QceF64Args {
   double shift = 0.0;
 };
 bool qce_f64_shape(int MP, int NP);
-int qce_f64_tile();
+int qce_f64_tile(int MP, int NP);  // samples per workgroup tile
 long long qce_pack_f64all_bytes(int MP, int NP, int has_mean);
 hipError_t qce_launch_pack_f64all(int K, int M, int N, int MP, int NP, int has_mean, const double2* Linv,
                                   const double2* W, const double2* q0, const double2* bvec, double* pack,

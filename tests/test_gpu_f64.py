@@ -140,3 +140,58 @@ def test_f64_device_io_matches_host():
     out = dm.estimate(torch.from_numpy(y).to("cuda"))
     dm.synchronize()
     assert rel_fro(out.cpu().numpy(), host) == 0.0
+
+
+@pytest.mark.parametrize("K,N,pilots,B,n_bits,mean", [
+    (256, 128, 1, 512, 1, False),    # cfg4 geometry at its full K (the selective-mode limit K = 256)
+    (24, 100, 1, 300, 2, True),      # padded N (100 -> 128), means
+    (12, 64, 2, 400, 1, False),      # two pilots: M = 128 over N = 64
+    (9, 128, 1, 200, np.inf, True),  # unquantised, means, N = 128
+])
+def test_f64_large_shapes_vs_oracle(K, N, pilots, B, n_bits, mean):
+    """FP64 fused kernel at padded dimensions of 128 (one column tile per wave)."""
+    _gpu_or_skip()
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import Gmm_nbit, inputs
+    means, covs, w = inputs.synthetic_model(K, N, seed=K + N)
+    rng = np.random.default_rng(K * N + 1)
+    if mean:
+        means = 0.3 * inputs.crandn(K, N, rng=rng)
+    h, _ = inputs.scm_generate(B, 1, N, rng, n_path=3)
+    h = h[:, 0, :].astype(complex)
+    A = None if pilots == 1 else inputs.get_pilot_matrix(N, pilots, n_bits)
+    qz = (None, None, None)
+    if n_bits not in (1, np.inf):
+        qz = inputs.uniform_quantizer(5.0, n_bits)
+    y = inputs.get_observation_nbit(h, 5.0, A, n_bits, qz[0], qz[1], rng=rng)
+    g = Gmm_nbit.from_params(means, covs, w)
+    hg = g.estimate_from_y(y, 5.0, N, A, "all", n_bits, "uniform", qz)
+    ho = O.estimate(means, covs, w, y, 5.0, N, A, "all", n_bits, "uniform", qz)
+    # 1 bit with two pilots: the arcsine law's sensitivity at |rho| ~ 1 (test_gpu_parity.py) bounds the tables
+    tol = 1e-7 if (pilots > 1 and n_bits == 1) else F64_TOL
+    assert rel_fro(hg, ho) < tol, rel_fro(hg, ho)
+
+
+@pytest.mark.parametrize("wg", ["1", "13", "300"])
+def test_f64_n128_stream_k_and_partial(wg, monkeypatch):
+    _gpu_or_skip()
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import _lib
+    from quantized_channel_estimation_amd.sharding import combine_packed_numpy
+    monkeypatch.setenv("QCE_WORKGROUPS", wg)
+    K, N, B = 30, 128, 333
+    means, covs, w, h, y, qz = _synthetic(K, N, B, 77, 1, mean=True)
+    ho = O.estimate(means, covs, w, y, 5.0, N, None, "all", 1)
+    dm = _lib.DeviceModel(means, covs, w)
+    dm.prepare(None, 5.0, 1.0)
+    assert rel_fro(dm.estimate(y), ho) < F64_TOL
+    parts = []
+    shift = None
+    models = []
+    for lo, hi in [(0, 11), (11, 30)]:
+        d = _lib.DeviceModel(means[lo:hi], covs[lo:hi], w[lo:hi])
+        d.prepare(None, 5.0, 1.0)
+        models.append(d)
+    shift = max(float(np.max(d.cconst())) for d in models)
+    parts = [d.partial_shifted(y, shift) for d in models]
+    assert rel_fro(combine_packed_numpy(parts), ho) < F64_TOL
