@@ -99,6 +99,9 @@ struct qce_model {
   DevBuf<double> fp_m, fp_s, fp_a;
   DevBuf<double> part_a64;  // FP64 partial accumulator behind the f32 qce_estimate_partial
   DevBuf<double> fp_pack;   // host-I/O staging of qce_estimate_partial_shifted
+  DevBuf<double> w64_scr;   // FP64 selection weights (selective modes)
+  DevBuf<double2> WT;       // transposed filters W_k^T for the FP64 selective-mode kernel (built lazily)
+  int wt_valid = 0;
   int cu_count = 256;
   // Fourier-domain path for (block-)circulant mixtures (qce_fft.hip): structure found at creation
   int fft_n1 = 0, fft_n2 = 0;
@@ -543,7 +546,8 @@ int qce_model_destroy(qce_model* m) {
   m->sp_a.release();
   m->yflag.release();
   m->pack_f64.release();
-  for (auto* b : {&m->fp_m, &m->fp_s, &m->fp_a, &m->part_a64, &m->fp_pack}) b->release();
+  for (auto* b : {&m->fp_m, &m->fp_s, &m->fp_a, &m->part_a64, &m->fp_pack, &m->w64_scr}) b->release();
+  m->WT.release();
   for (auto* b : {&m->f_ceig, &m->f_rinvT, &m->f_cprime, &m->f_wT, &m->f_gain}) b->release();
   for (auto* b : {&m->f_col0, &m->f_mspec, &m->f_uT, &m->f_bT}) b->release();
   m->f_bad.release();
@@ -808,6 +812,7 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
   p.stride64 = s64;
   m->pack_args = p;
   m->packs_valid = 0;
+  m->wt_valid = 0;
   p.pack32 = nullptr;  // selective-mode / log-prob tables are packed on first use (ensure_packs)
   p.pack64 = nullptr;
   HIPCHK(qce_launch_prepare(p, st));
@@ -923,8 +928,17 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
     HIPCHK(m->lp_scr.ensure((size_t)B * m->K));
     HIPCHK(m->w_scr.ensure((size_t)B * m->K));
     HIPCHK(qce_launch_lp(a, m->lp_scr.p, st));
-    HIPCHK(qce_launch_select(B, m->K, m->lp_scr.p, kmode, n, p, nullptr, nullptr, m->w_scr.p, st));
-    HIPCHK(qce_launch_est_weighted(a, m->w_scr.p, dh, st));
+    if (want_f64(m)) {  // FP64 selection weights and FP64 filters (the reference's complex128 arithmetic)
+      HIPCHK(m->w64_scr.ensure((size_t)B * m->K));
+      HIPCHK(qce_launch_select(B, m->K, m->lp_scr.p, kmode, n, p, nullptr, nullptr, nullptr, st, m->w64_scr.p));
+      HIPCHK(m->WT.ensure((size_t)m->K * m->M * m->N));
+      HIPCHK(qce_launch_sparse_f64(B, m->N, m->M, m->K, dy, m->w64_scr.p, m->W.p, m->bvec.p, m->WT.p, !m->wt_valid,
+                                   dh, st));
+      m->wt_valid = 1;
+    } else {
+      HIPCHK(qce_launch_select(B, m->K, m->lp_scr.p, kmode, n, p, nullptr, nullptr, m->w_scr.p, st));
+      HIPCHK(qce_launch_est_weighted(a, m->w_scr.p, dh, st));
+    }
   }
   if (io == QCE_IO_HOST) {
     HIPCHK(hipMemcpyAsync(h_out, dh, sizeof(double2) * (size_t)B * m->N, hipMemcpyDeviceToHost, st));

@@ -288,7 +288,7 @@ QCE_DEV void wave_argmax(double& v, int& idx, bool prefer_low) {
 
 __global__ __launch_bounds__(256) void k_select(long long B, int K, const double* __restrict__ lp, int mode, int nsel,
                                                 double psel, double* __restrict__ proba, long long* __restrict__ labels,
-                                                float* __restrict__ wts) {
+                                                float* __restrict__ wts, double* __restrict__ wts64) {
   const int lane = threadIdx.x & 63;
   const long long b = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
@@ -328,12 +328,12 @@ __global__ __launch_bounds__(256) void k_select(long long B, int K, const double
     for (int i = 0; i < 4; ++i)
       if (lane + 64 * i < K) proba[b * K + lane + 64 * i] = pr[i];
   }
-  if (!wts) return;
-  float w[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (!wts && !wts64) return;
+  double w[4] = {0.0, 0.0, 0.0, 0.0};
   if (mode == 3 || (mode == 1 && nsel == 1)) {  // argmax path (:200-207): h = h_label, weight exactly 1
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if (lane + 64 * i == bi) w[i] = 1.0f;
+      if (lane + 64 * i == bi) w[i] = 1.0;
   } else if (mode == 1 || mode == 2) {
     // descending-proba selection (:213 / :235-236); ties broken towards the higher index,
     // matching a reversed stable ascending sort
@@ -368,11 +368,14 @@ __global__ __launch_bounds__(256) void k_select(long long B, int K, const double
     tot = wave_sum(tot);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      if ((taken >> i) & 1) w[i] = (float)(chosen[i] / tot);
+      if ((taken >> i) & 1) w[i] = chosen[i] / tot;
   }
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    if (lane + 64 * i < K) wts[b * K + lane + 64 * i] = w[i];
+    if (lane + 64 * i < K) {
+      if (wts) wts[b * K + lane + 64 * i] = (float)w[i];
+      if (wts64) wts64[b * K + lane + 64 * i] = w[i];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -469,9 +472,79 @@ hipError_t qce_launch_lp(const QceEstArgs& a, double* lp, hipStream_t st) {
 }
 
 hipError_t qce_launch_select(long long B, int K, const double* lp, int mode, int n, double p, double* proba,
-                             long long* labels, float* wts, hipStream_t st) {
+                             long long* labels, float* wts, hipStream_t st, double* wts64) {
   if (K > 256) return hipErrorInvalidValue;
   dim3 grid((unsigned)((B + 3) / 4));
-  hipLaunchKernelGGL(k_select, grid, dim3(256), 0, st, B, K, lp, mode, n, p, proba, labels, wts);
+  hipLaunchKernelGGL(k_select, grid, dim3(256), 0, st, B, K, lp, mode, n, p, proba, labels, wts, wts64);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// FP64 selective-mode LMMSE (gmm_cplx_bussgang.py:200-219, :229-242): h_b = sum_k w_bk (W_k y_b + b_k) over the
+// components the selection kept (w_bk != 0, wave-uniform skip), FP64 VALU.  One wave per sample, y in LDS,
+// filters transposed (WT_k = W_k^T, M x N) so the 64 lanes (output rows) read one coalesced 1 KB row per m.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_est_sparse_f64(long long B, int N, int M, int K, const double2* __restrict__ y,
+                                                        const double* __restrict__ w, const double2* __restrict__ WT,
+                                                        const double2* __restrict__ bvec, double2* __restrict__ h) {
+  __shared__ double2 ys[4][256];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long b = (long long)blockIdx.x * 4 + wv;
+  const bool live = b < B;
+  if (live)
+    for (int m = lane; m < M; m += 64) ys[wv][m] = y[b * M + m];
+  __syncthreads();
+  if (!live) return;
+  double2 acc[4];  // rows n = lane + 64 r (N <= 256)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc[r] = make_double2(0.0, 0.0);
+  const double* wr = w + b * K;
+  for (int k = 0; k < K; ++k) {
+    const double wk = wr[k];
+    if (wk == 0.0) continue;  // same value in every lane of the wave
+    const double2* Wk = WT + (long long)k * M * N;
+    double2 t[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) t[r] = (lane + 64 * r < N) ? bvec[(long long)k * N + lane + 64 * r] : make_double2(0.0, 0.0);
+    for (int m = 0; m < M; ++m) {
+      const double2 ym = ys[wv][m];
+      const double2* row = Wk + (long long)m * N;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (lane + 64 * r < N) t[r] = cfma(row[lane + 64 * r], ym, t[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      acc[r].x = fma(wk, t[r].x, acc[r].x);
+      acc[r].y = fma(wk, t[r].y, acc[r].y);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    if (lane + 64 * r < N) h[b * N + lane + 64 * r] = acc[r];
+}
+
+// WT_k[m][n] = W_k[n][m]
+__global__ __launch_bounds__(256) void k_transpose_w(int K, int N, int M, const double2* __restrict__ W,
+                                                     double2* __restrict__ WT) {
+  const long long total = (long long)K * N * M;
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const long long k = e / ((long long)M * N), r = e % ((long long)M * N);
+    const int m = (int)(r / N), n = (int)(r % N);
+    WT[e] = W[(k * N + n) * M + m];
+  }
+}
+
+hipError_t qce_launch_sparse_f64(long long B, int N, int M, int K, const double2* y, const double* w, const double2* W,
+                                 const double2* bvec, double2* WT, bool transpose, double2* h, hipStream_t st) {
+  if (N > 256 || M > 256) return hipErrorInvalidValue;
+  if (transpose) {
+    long long blocks = ((long long)K * N * M + 255) / 256;
+    blocks = blocks > 16384 ? 16384 : blocks;
+    hipLaunchKernelGGL(k_transpose_w, dim3((unsigned)blocks), dim3(256), 0, st, K, N, M, W, WT);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_est_sparse_f64, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, N, M, K, y, w, WT, bvec, h);
   return hipGetLastError();
 }

@@ -48,7 +48,11 @@ hipError_t qce_launch_est_partial(const QceEstArgs& a, double* m, double* s, flo
 hipError_t qce_launch_lp(const QceEstArgs& a, double* lp, hipStream_t st);
 // selection: mode 0 = proba only, 1 = top-n, 2 = cumulative-p, 3 = argmax(lp)
 hipError_t qce_launch_select(long long B, int K, const double* lp, int mode, int n, double p, double* proba,
-                             long long* labels, float* wts, hipStream_t st);
+                             long long* labels, float* wts, hipStream_t st, double* wts64 = nullptr);
+// FP64 selective-mode LMMSE h = sum_k w64[b][k] (W_k y + b_k), w64 sparse; WT (K x M x N) = transposed filters
+// (built from W when transpose, else reused)
+hipError_t qce_launch_sparse_f64(long long B, int N, int M, int K, const double2* y, const double* w, const double2* W,
+                                 const double2* bvec, double2* WT, bool transpose, double2* h, hipStream_t st);
 // h = sum_k wts[b][k] (W_k y_b + b_k)
 hipError_t qce_launch_est_weighted(const QceEstArgs& a, const float* wts, double2* h, hipStream_t st);
 bool qce_shape_supported(int MP, int NP);         // FP32 fused kernel (M, N <= 64)

@@ -105,7 +105,9 @@ def _mode_of(n_summands_or_proba, K):
 
 def _nbits_of(n_bits):
     if isinstance(n_bits, str):
-        raise NotImplementedError("n_bits must be a number or np.inf (the reference's prepare does not accept 'inf')")
+        # the reference's prepare compares the string with an int (uniform_quantizer.py via :281) and raises
+        # this TypeError (golden: tests/golden/quirks.npz str_inf)
+        raise TypeError("'<=' not supported between instances of 'str' and 'int'")
     return float(n_bits)
 
 
@@ -338,7 +340,8 @@ class Gmm_nbit:
         """gmm_cplx_bussgang.py:166-243 — returns h_est (B, N) complex128."""
         y = np.asarray(y)
         if y.ndim != 2:
-            raise ValueError("y must be a 2D array (B, M)")  # the reference fails at :405 for 1-D y
+            # the reference unpacks y.shape at :405 (golden: tests/golden/quirks.npz y1d)
+            raise ValueError(f"not enough values to unpack (expected 2, got {y.ndim})")
         N = self.covs_cplx.shape[-1]
         if A is not None:
             A = np.asarray(A)

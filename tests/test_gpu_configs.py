@@ -1,0 +1,82 @@
+"""BASELINE.json configurations at their own model sizes (full K), through the C-ABI, against the
+FP64 oracle: cfg4 (K=256, N=128, 'full', 1 bit) and cfg5 (K=128, N=256, block-circulant (4, 64),
+2-bit uniform) — every mode, the Fourier path and the dense path, and the K-shard partials that
+the multi-GPU split all-reduces.  Batches are reduced (the oracle's 'all' mode materialises
+B x K x N filter outputs); the full batch sizes run in bench.py with parity on 512 samples."""
+import numpy as np
+import pytest
+
+from conftest import rel_fro
+
+pytestmark = pytest.mark.gpu
+
+F64_TOL = 1e-9
+H_TOL = 1e-5
+
+
+def _inputs(K, N, B, cov, blocks, n_bits, seed):
+    from quantized_channel_estimation_amd import inputs
+    means, covs, w = inputs.synthetic_model(K, N, cov_type=cov, blocks=blocks)
+    rng = np.random.default_rng(seed)
+    h, _ = inputs.scm_generate(B, 1, N, rng, n_path=3)
+    h = h[:, 0, :].astype(complex)
+    qz = (None, None, None)
+    if n_bits not in (1, np.inf):
+        qz = inputs.get_quantizer([5.0], n_bits, "uniform")[5.0]
+    y = inputs.get_observation_nbit(h, 5.0, None, n_bits, qz[0], qz[1], rng=rng)
+    return means, covs, w, h, y, qz
+
+
+def _shard_combine(means, covs, w, y, n_bits, cuts):
+    from quantized_channel_estimation_amd import _lib
+    from quantized_channel_estimation_amd.sharding import combine_packed_numpy
+    models = []
+    for lo, hi in cuts:
+        d = _lib.DeviceModel(means[lo:hi], covs[lo:hi], w[lo:hi])
+        d.prepare(None, 5.0, float(n_bits))
+        models.append(d)
+    shift = max(float(np.max(d.cconst())) for d in models)
+    return combine_packed_numpy([d.partial_shifted(y, shift) for d in models])
+
+
+def test_cfg4_all_modes_and_kshard():
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import Gmm_nbit
+    K, N, B = 256, 128, 1024
+    means, covs, w, h, y, qz = _inputs(K, N, B, "full", None, 1, 4004)
+    g = Gmm_nbit.from_params(means, covs, w)
+    for mode, tol in (("all", F64_TOL), (1, F64_TOL), (3, F64_TOL), (0.9, F64_TOL)):
+        hg = g.estimate_from_y(y, 5.0, N, None, mode, 1)
+        ho = O.estimate(means, covs, w, y, 5.0, N, None, mode, 1)
+        assert rel_fro(hg, ho) < tol, (mode, rel_fro(hg, ho))
+        if mode == "all":
+            h_all = ho
+    t = O.prepare(means, covs, np.eye(N), 5.0, 1)
+    np.testing.assert_array_equal(g._predict_cplx(y), O.predict(y, t["means_y"], t["P"], w))
+    # K shards of the north-star split (2 and 8 ranks' worth of components)
+    for cuts in ([(0, 128), (128, 256)], [(32 * r, 32 * r + 32) for r in range(8)]):
+        assert rel_fro(_shard_combine(means, covs, w, y, 1, cuts), h_all) < F64_TOL
+
+
+@pytest.mark.parametrize("fft", ["1", "0"])
+def test_cfg5_fourier_and_dense(fft, monkeypatch):
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import Gmm_nbit
+    monkeypatch.setenv("QCE_FFT", fft)
+    K, N, B = 128, 256, 256
+    means, covs, w, h, y, qz = _inputs(K, N, B, "block-circulant", (4, 64), 2, 5005)
+    g = Gmm_nbit.from_params(means, covs, w)
+    for mode in ("all", 1, 3, 0.9):
+        hg = g.estimate_from_y(y, 5.0, N, None, mode, 2, "uniform", qz)
+        assert g._dev.structure()[2] == (1 if fft == "1" else 0)
+        ho = O.estimate(means, covs, w, y, 5.0, N, None, mode, 2, "uniform", qz)
+        # Fourier path: FP64 throughout ('all'); selective modes carry its fp32 selection weights.  Dense
+        # N = 256: 'all' runs the fp16-split kernel (no FP64 fused instance at 256), selective modes FP64.
+        if fft == "1":
+            tol = 1e-9 if mode == "all" else 1e-6
+        else:
+            tol = H_TOL if mode == "all" else F64_TOL
+        assert rel_fro(hg, ho) < tol, (fft, mode, rel_fro(hg, ho))
+    h_all = O.estimate(means, covs, w, y, 5.0, N, None, "all", 2, "uniform", qz)
+    tol = 1e-6 if fft == "1" else H_TOL  # the Fourier / fp16-split partials carry an f32 accumulator
+    assert rel_fro(_shard_combine(means, covs, w, y, 2, [(0, 64), (64, 128)]), h_all) < tol

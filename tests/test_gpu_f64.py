@@ -195,3 +195,35 @@ def test_f64_n128_stream_k_and_partial(wg, monkeypatch):
     shift = max(float(np.max(d.cconst())) for d in models)
     parts = [d.partial_shifted(y, shift) for d in models]
     assert rel_fro(combine_packed_numpy(parts), ho) < F64_TOL
+
+
+@pytest.mark.parametrize("K,N,pilots,B,n_bits,mean", [
+    (128, 64, 1, 1024, 1, False),    # metric geometry
+    (33, 48, 1, 700, 2, True),       # padded, means, 2-bit
+    (64, 128, 1, 300, 1, False),     # N = 128
+    (6, 64, 2, 300, 1, True),        # two pilots (M = 128)
+    (5, 256, 1, 120, 1, False),      # N = 256
+])
+def test_f64_selective_modes_vs_oracle(K, N, pilots, B, n_bits, mean):
+    """Modes 1 (argmax), top-n and cumulative-p in FP64: FP64 log-probabilities (exact labels), FP64
+    selection weights and FP64 filters (k_est_sparse_f64) — the reference's complex128 arithmetic."""
+    _gpu_or_skip()
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import Gmm_nbit, inputs
+    means, covs, w = inputs.synthetic_model(K, N, seed=K + 2 * N)
+    rng = np.random.default_rng(K + N + 5)
+    if mean:
+        means = 0.3 * inputs.crandn(K, N, rng=rng)
+    h, _ = inputs.scm_generate(B, 1, N, rng, n_path=3)
+    h = h[:, 0, :].astype(complex)
+    A = None if pilots == 1 else inputs.get_pilot_matrix(N, pilots, n_bits)
+    qz = (None, None, None)
+    if n_bits not in (1, np.inf):
+        qz = inputs.uniform_quantizer(5.0, n_bits)
+    y = inputs.get_observation_nbit(h, 5.0, A, n_bits, qz[0], qz[1], rng=rng)
+    g = Gmm_nbit.from_params(means, covs, w)
+    tol = 1e-7 if (pilots > 1 and n_bits == 1) else F64_TOL
+    for mode in (1, 3, 0.9, K + 5):
+        hg = g.estimate_from_y(y, 5.0, N, A, mode, n_bits, "uniform", qz)
+        ho = O.estimate(means, covs, w, y, 5.0, N, A, mode, n_bits, "uniform", qz)
+        assert rel_fro(hg, ho) < tol, (mode, rel_fro(hg, ho))
