@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="metric", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0, help="override B (observations per step)")
+    ap.add_argument("--components", type=int, default=0, help="override K (PMC calibration runs)")
     ap.add_argument("--shard", default=None, choices=["batch", "k"])
     ap.add_argument("--precision", default="f64", choices=["f64", "fast"],
                     help="dense 'all' arithmetic: f64 (the reference's complex128, default) or fast (fp16 split)")
@@ -329,6 +330,8 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     if args.batch:
         cfg["B"] = args.batch
+    if args.components:
+        cfg["K"] = args.components
     K, N, B = cfg["K"], cfg["N"], cfg["B"]
     data_seed = rank if args.shard == "batch" else 0
     means, covs, w, h, y, quantizer = make_inputs(cfg, data_seed)

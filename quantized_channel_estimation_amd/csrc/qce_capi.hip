@@ -177,6 +177,11 @@ bool use_h2() {
   return !(e && strcmp(e, "f32") == 0);
 }
 
+#ifdef QCE_STAMPS
+unsigned long long* g_f64_stamps = nullptr;  // diagnostic build: segment cycles of the last FP64 launch
+long long g_f64_stamp_records = 0;
+#endif
+
 // Arithmetic of the dense 'all' / partial path for this model: the model option, overridden by
 // QCE_KERNEL=f64 | h2 | f32 (A/B runs).
 bool want_f64(const qce_model* m) {
@@ -233,6 +238,18 @@ int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om
   a.pa = m->fp_a.p;
   a.pk = pk;
   a.shift = shift;
+  {
+    const char* wv = getenv("QCE_F64_WAVES");  // 8 (default): two waves per SIMD where M, N <= 64
+    a.waves = (wv && atoi(wv) == 4) ? 4 : 8;
+  }
+#ifdef QCE_STAMPS
+  static unsigned long long* g_stamps = nullptr;
+  if (!g_stamps) HIPCHK(hipMalloc(&g_stamps, sizeof(unsigned long long) * 4096 * 8 * 8));
+  HIPCHK(hipMemsetAsync(g_stamps, 0, sizeof(unsigned long long) * 4096 * 8 * 8, st));
+  a.stamps = nwg <= 4096 ? g_stamps : nullptr;
+  g_f64_stamps = g_stamps;
+  g_f64_stamp_records = nwg * a.waves;
+#endif
   HIPCHK(qce_launch_est_f64(a, h == nullptr, st));
   return QCE_OK;
 }
@@ -1646,3 +1663,14 @@ int qce_synchronize(qce_model* m) {
 }
 
 }  // extern "C"
+
+#ifdef QCE_STAMPS
+// diagnostic build only: per-wave segment cycles (8 per wave) of the last k_est_all_f64 launch
+extern "C" int qce_debug_f64_stamps(unsigned long long* out, long long n) {
+  if (!g_f64_stamps) return QCE_ESTATE;
+  if (n > g_f64_stamp_records * 8) n = g_f64_stamp_records * 8;
+  if (hipDeviceSynchronize() != hipSuccess) return QCE_EHIP;
+  if (hipMemcpy(out, g_f64_stamps, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost) != hipSuccess) return QCE_EHIP;
+  return (int)n;
+}
+#endif

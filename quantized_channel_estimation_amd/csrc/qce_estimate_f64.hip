@@ -128,11 +128,7 @@ __global__ __launch_bounds__(64) void k_pack_f64all(int M, int N, int MP, int NP
 // host side
 // ---------------------------------------------------------------------------
 namespace {
-int blocks_per_comp(int MP, int NP, int hm) {
-  const int NTL = MP / 8, NTW = NP / 8, KP = MP / 4, HMI = hm ? 1 : 0;
-  const int n = NTL * (NTL + 1) + HMI * NTL + NTW * (KP + HMI);
-  return (n + 15) / 16 * 16;
-}
+int blocks_per_comp(int MP, int NP, int hm) { return f64_bpc(f64_blocks(MP, NP, hm ? 1 : 0)); }
 }  // namespace
 
 bool qce_f64_shape(int MP, int NP) {

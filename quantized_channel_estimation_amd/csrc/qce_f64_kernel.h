@@ -37,6 +37,28 @@
 
 namespace {
 
+// Ring geometry: chunks of CB blocks (1 KB each), NSLOT chunks of LDS.  One barrier per chunk, so CB is as large
+// as the LDS allows (NSLOT >= 3, <= 144 KB) unless the per-component padding to whole chunks costs more load
+// traffic than the barriers it saves; CB is a multiple of 8 (whole pieces per wave for 4 and 8 waves).
+constexpr __host__ __device__ int f64_blocks(int MP, int NP, int hmi) {
+  return (MP / 8) * (MP / 8 + 1) + hmi * (MP / 8) + (NP / 8) * (MP / 4 + hmi);
+}
+constexpr __host__ __device__ int f64_cb(int n) {
+  int best = 16;
+  double best_cost = 1e30;
+  for (int cb = 16; cb <= 48; cb += 8) {
+    const int pad = (n + cb - 1) / cb * cb - n;
+    const double cost = (double)pad / n + 2.0 / cb;
+    if (cost < best_cost - 1e-12) {
+      best_cost = cost;
+      best = cb;
+    }
+  }
+  return best;
+}
+constexpr __host__ __device__ int f64_nslot(int cb) { return 144 / cb < 8 ? 144 / cb : 8; }
+constexpr __host__ __device__ int f64_bpc(int n) { return (n + f64_cb(n) - 1) / f64_cb(n) * f64_cb(n); }
+
 template <int MP, int NP, bool HM>
 struct F64G {
   static constexpr int NTL = MP / 8;  // GL row tiles (16 real rows = 8 complex rows)
@@ -46,14 +68,14 @@ struct F64G {
   static constexpr int GL_BLOCKS = NTL * (NTL + 1) + HMI * NTL;
   static constexpr int GW_BLOCKS = NTW * (KP + HMI);
   static constexpr int BLOCKS = GL_BLOCKS + GW_BLOCKS;
-  static constexpr int CB = 16;  // blocks per ring chunk (16 KB)
-  static constexpr int BPC = (BLOCKS + CB - 1) / CB * CB;
+  static constexpr int CB = f64_cb(BLOCKS);  // blocks per ring chunk
+  static constexpr int NSLOT = f64_nslot(CB);
+  static constexpr int CHUNK = CB * 1024;
+  static constexpr int BPC = f64_bpc(BLOCKS);
   static constexpr int CPC = BPC / CB;
+  static_assert(BLOCKS == f64_blocks(MP, NP, HMI), "block count");
   static constexpr __host__ __device__ int gl_off(int T) { return T * (T + 1) + HMI * T; }
 };
-
-constexpr int F64_NSLOT = 8;                // ring slots (128 KB of LDS)
-constexpr int F64_CHUNK = 16 * 1024;
 
 // block b of a component -> kind (0 GL data, 1 GL mean, 2 GW data, 3 GW mean, 4 pad), tile T, k-pair s
 struct BlockInfo {
@@ -73,6 +95,28 @@ constexpr BlockInfo block_info(int b) {
   if (r < (G::KP + G::HMI) * G::NTW) return BlockInfo{3, r - G::KP * G::NTW, G::KP};
   return BlockInfo{4, 0, 0};
 }
+
+// Diagnostic build only (-DQCE_STAMPS): per-wave cycle sums of the kernel's segments (s_memtime), stored
+// by lane 0 into a buffer of their own (qce_debug_f64_stamps); the product kernel executes no stamp.
+#ifdef QCE_STAMPS
+#define F64_STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime();
+#define F64_STAMP(i)                                     \
+  do {                                                   \
+    __builtin_amdgcn_sched_barrier(0);                   \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   \
+    st_acc[(i)] += t_ - st_prev;                         \
+    st_prev = t_;                                        \
+    __builtin_amdgcn_sched_barrier(0);                   \
+  } while (0)
+#define F64_STAMP_FLUSH                                                                    \
+  if (stamps && lane == 0)                                                                 \
+    for (int i_ = 0; i_ < 8; ++i_) stamps[((long long)blockIdx.x * NW + wave) * 8 + i_] = st_acc[i_];
+#else
+#define F64_STAMP_DECL
+#define F64_STAMP(i)
+#define F64_STAMP_FLUSH
+#endif
 
 template <int N_>
 QCE_DEV void wait_vmcnt() {
@@ -116,18 +160,6 @@ struct RingCursor {
   }
 };
 
-// one chunk = 16 wave-instructions of 1 KB, LPW per wave (wave-uniform addresses, no branches)
-template <int NW>
-QCE_DEV void issue_chunk(const char* __restrict__ src, char* dst, int wave, int lane) {
-  constexpr int LPW = (F64_CHUNK / 1024) / NW;
-  src += wave * 1024 + lane * 16;
-  dst += wave * 1024;
-#pragma unroll
-  for (int i = 0; i < LPW; ++i)
-    __builtin_amdgcn_global_load_lds((const void*)(src + i * NW * 1024),
-                                     (__attribute__((address_space(3))) void*)(dst + i * NW * 1024), 16, 0, 0);
-}
-
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -140,14 +172,15 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
                                                          double* __restrict__ om, double* __restrict__ os,
                                                          double* __restrict__ oa, double* __restrict__ pm,
                                                          double* __restrict__ ps, double* __restrict__ pa,
-                                                         double* __restrict__ pk, double shift) {
+                                                         double* __restrict__ pk, double shift,
+                                                         unsigned long long* __restrict__ stamps) {
   using G = F64G<MP, NP, HM>;
   constexpr int TS = NW * 16 * CT;           // samples per tile
-  constexpr int LPW = (F64_CHUNK / 1024) / NW;  // global_load_lds per wave per chunk
+  constexpr int LPW = G::CB / NW;  // global_load_lds per wave per chunk
   constexpr int E = 2;                        // boundary lead (blocks) = LDS prefetch distance
   constexpr double RESCALE = 32.0;            // lazy max: rescale only when lp exceeds m by this
-  static_assert((F64_CHUNK / 1024) % NW == 0, "chunk split");
-  __shared__ __attribute__((aligned(16))) char lds[F64_NSLOT * F64_CHUNK];
+  static_assert(G::CB % NW == 0, "chunk split");
+  __shared__ __attribute__((aligned(16))) char lds[G::NSLOT * G::CHUNK];
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -163,29 +196,45 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
   const long long t_first = tail0 + (L > 0 ? item0 / K : 0);
   const long long nseg = (long long)R + (ntail > 0 ? (item1 - 1) / K - item0 / K + 1 : 0);
 
+  F64_STAMP_DECL
   // ---- ring ----
   RingCursor cur;
   cur.init(R * K, (int)(item0 % K), (int)ntail, K, G::CPC);
   int issued = 0;  // chunks issued so far (stream index of the next one)
-  auto issue_next = [&]() {
-    const char* src = pack + cur.chunk_index() * (long long)F64_CHUNK;
-    char* dst = lds + (issued & (F64_NSLOT - 1)) * F64_CHUNK;
-    issue_chunk<NW>(src, dst, wave, lane);
+  // A chunk refill is LPW global_load_lds pieces of 1 KB per wave.  refill_begin fixes the chunk's source and
+  // slot; the pieces go out one per MFMA gap of the block that follows the barrier (an LDS-DMA issue among
+  // bare MFMAs costs ~60 cycles — issued back to back after the barrier they left the MFMA pipe idle).
+  const char* rsrc = pack;
+  int rdst = 0;
+  auto refill_begin = [&]() {
+    rsrc = pack + cur.chunk_index() * (long long)G::CHUNK + wave * 1024 + lane * 16;
+    rdst = (issued % G::NSLOT) * G::CHUNK + wave * 1024;
     cur.advance();
     ++issued;
   };
-  // boundary for stream chunk jn: its loads landed everywhere, and every wave is done with chunk
-  // jn - 2, whose slot is refilled with chunk jn + NSLOT - 2
-  auto boundary = [&]() {
-    wait_vmcnt<(F64_NSLOT - 3) * LPW>();
+  auto refill_pieces = [&](int lo, int hi) {
+    for (int i = lo; i < hi; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(rsrc + i * NW * 1024),
+                                       (__attribute__((address_space(3))) void*)(lds + rdst + i * NW * 1024), 16, 0,
+                                       0);
+  };
+  // boundary for stream chunk jn: its loads landed everywhere, and every wave is done with chunk jn - 2,
+  // whose slot is refilled (refill_begin + pieces) with chunk jn + NSLOT - 2
+  auto boundary_wait = [&]() {
+    wait_vmcnt<(G::NSLOT - 3) * LPW>();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    issue_next();
+    F64_STAMP(3);
   };
 #pragma unroll 1
-  for (int j = 0; j < F64_NSLOT - 2; ++j) issue_next();
-  boundary();  // chunk 0
+  for (int j = 0; j < G::NSLOT - 2; ++j) {
+    refill_begin();
+    refill_pieces(0, LPW);
+  }
+  boundary_wait();  // chunk 0
+  refill_begin();
+  refill_pieces(0, LPW);
   int cstream = 0;  // stream index of the current component's chunk 0
 
   for (long long seg = 0; seg < nseg; ++seg) {
@@ -202,7 +251,6 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
       khi = (int)((tK + K < item1 ? tK + K : item1) - tK);
     }
     const long long sbase = t * TS + (long long)wave * 16 * CT;
-    // y fragments: k-pair s, lane group g -> complex column 4s + g (re: k-step 2s, im: 2s+1)
     // y fragments: k-pair s, lane group g -> complex column 4s + g (re: k-step 2s, im: 2s+1).  Rows past B
     // and columns past M are clamped (finite values of the same tensor) instead of masked: a padded column
     // meets zero table entries, an invalid sample is never written.  The laundered lane constants keep the
@@ -222,6 +270,7 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
       }
     }
     wait_vmcnt<0>();
+    F64_STAMP(5);
     f64x4 out[G::NTW][CT];
 #pragma unroll
     for (int T = 0; T < G::NTW; ++T)
@@ -237,14 +286,14 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
 #pragma unroll 1
     for (int k = klo; k < khi; ++k) {
       const double ck = cconst[k];
-      const int slot0 = cstream & (F64_NSLOT - 1);
+      const int slot0 = cstream % G::NSLOT;
       // LDS offset of this lane's 16 B in the slot of the chunk being read; advanced when the reads cross
       // into the next chunk and laundered, so the compiler keeps one live offset instead of hoisting one
       // per chunk of the unrolled component
       int rslot = slot0;
-      int roff = lane * 16 + rslot * F64_CHUNK;
+      int roff = lane * 16 + rslot * G::CHUNK;
       auto rd = [&](int off) -> double2 { return *reinterpret_cast<const double2*>(&lds[roff + off]); };
-      f64x4 acc[CT];
+      f64x4 acc[CT], accp[CT];
       double qp[CT], p[CT];
       double bs0[CT], bs1[CT];
 #pragma unroll
@@ -253,7 +302,19 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
         p[c] = 0.0;
         bs0[c] = bs1[c] = 0.0;
         acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
+        accp[c] = acc[c];
       }
+      auto fold = [&](f64x4 (&x)[CT]) {
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          qp[c] = fma(x[c][0], x[c][0], qp[c]);
+          qp[c] = fma(x[c][1], x[c][1], qp[c]);
+          qp[c] = fma(x[c][2], x[c][2], qp[c]);
+          qp[c] = fma(x[c][3], x[c][3], qp[c]);
+          // pin the fold here: sunk to the softmax, every row tile would keep its own accumulators
+          asm volatile("" : "+v"(qp[c]));
+        }
+      };
       double2 buf[E + 1];
 #pragma unroll
       for (int i = 0; i < E; ++i) buf[i] = rd(i * 1024);
@@ -263,26 +324,51 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
             constexpr BlockInfo bi = block_info<MP, NP, HM>(b);
             __builtin_amdgcn_sched_barrier(0);  // keep the explicit prefetch distance (no LDS read hoisting)
             // next chunk's boundary E blocks early (the last one is the next component's chunk 0)
-            if constexpr ((b + E) % G::CB == 0) boundary();
+            constexpr bool RB = (b + E) % G::CB == 0;
+            if constexpr (RB) {
+              F64_STAMP(bi.kind <= 1 ? 0 : 2);
+              boundary_wait();
+              refill_begin();
+            }
             if constexpr (b + E < G::BPC) {
               constexpr int r = b + E;
               if constexpr (r % G::CB == 0) {
-                rslot = (rslot + 1) & (F64_NSLOT - 1);
-                roff = lane * 16 + rslot * F64_CHUNK;
+                rslot = rslot + 1 == G::NSLOT ? 0 : rslot + 1;
+                roff = lane * 16 + rslot * G::CHUNK;
                 asm volatile("" : "+v"(roff));
               }
               buf[r % (E + 1)] = rd((r % G::CB) * 1024);
             }
             const double2 a = buf[b % (E + 1)];
+            // MFMAs of this block; on a boundary step the refill pieces are spread over their gaps
+            constexpr int NMF = (bi.kind == 0 || bi.kind == 2) ? 2 * CT : (bi.kind == 4 ? 0 : CT);
+            int jm = 0;
+            auto gap = [&]() {
+              if constexpr (RB && NMF > 0) {
+                __builtin_amdgcn_sched_barrier(0);
+                refill_pieces(jm * LPW / NMF, (jm + 1) * LPW / NMF);
+                __builtin_amdgcn_sched_barrier(0);
+              }
+              ++jm;
+            };
             if constexpr (bi.kind == 0) {  // GL data: u += E(Linv) y over k-pair s
 #pragma unroll
-              for (int c = 0; c < CT; ++c) acc[c] = mfma16x16x4d(a.x, yv[c][bi.s].x, acc[c]);
+              for (int c = 0; c < CT; ++c) {
+                acc[c] = mfma16x16x4d(a.x, yv[c][bi.s].x, acc[c]);
+                gap();
+              }
 #pragma unroll
-              for (int c = 0; c < CT; ++c) acc[c] = mfma16x16x4d(a.y, yv[c][bi.s].y, acc[c]);
+              for (int c = 0; c < CT; ++c) {
+                acc[c] = mfma16x16x4d(a.y, yv[c][bi.s].y, acc[c]);
+                gap();
+              }
             } else if constexpr (bi.kind == 1) {  // GL mean column (-q0): B = 1 in lane group 0
               const double one = g == 0 ? 1.0 : 0.0;
 #pragma unroll
-              for (int c = 0; c < CT; ++c) acc[c] = mfma16x16x4d(a.x, one, acc[c]);
+              for (int c = 0; c < CT; ++c) {
+                acc[c] = mfma16x16x4d(a.x, one, acc[c]);
+                gap();
+              }
             } else if constexpr (bi.kind == 2) {  // GW data: out += E(W) (p y) over k-pair s
               if constexpr (bi.T == 0) {
 #pragma unroll
@@ -292,31 +378,44 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
                 }
               }
 #pragma unroll
-              for (int c = 0; c < CT; ++c) out[bi.T][c] = mfma16x16x4d(a.x, bs0[c], out[bi.T][c]);
+              for (int c = 0; c < CT; ++c) {
+                out[bi.T][c] = mfma16x16x4d(a.x, bs0[c], out[bi.T][c]);
+                gap();
+              }
 #pragma unroll
-              for (int c = 0; c < CT; ++c) out[bi.T][c] = mfma16x16x4d(a.y, bs1[c], out[bi.T][c]);
+              for (int c = 0; c < CT; ++c) {
+                out[bi.T][c] = mfma16x16x4d(a.y, bs1[c], out[bi.T][c]);
+                gap();
+              }
             } else if constexpr (bi.kind == 3) {  // GW mean column (b): B = p in lane group 0
 #pragma unroll
-              for (int c = 0; c < CT; ++c) out[bi.T][c] = mfma16x16x4d(a.x, g == 0 ? p[c] : 0.0, out[bi.T][c]);
+              for (int c = 0; c < CT; ++c) {
+                out[bi.T][c] = mfma16x16x4d(a.x, g == 0 ? p[c] : 0.0, out[bi.T][c]);
+                gap();
+              }
             }
-            // end of a GL row tile: fold its squares into the quad form
+            if constexpr (RB && NMF == 0) refill_pieces(0, LPW);
+            // GL row tiles: the squares of tile T are folded into the quad form one block later (after the
+            // first MFMAs of tile T+1 are issued, so the fold does not wait on tile T's last MFMA); the last
+            // tile folds at once, the softmax needs it
             if constexpr (bi.kind == 0 || bi.kind == 1) {
+              constexpr bool first = bi.kind == 0 && bi.s == 0;
+              if constexpr (first && bi.T > 0) fold(accp);
               constexpr bool last = HM ? (bi.kind == 1) : (bi.s == 2 * bi.T + 1);
               if constexpr (last) {
+                if constexpr (bi.T == G::NTL - 1) {
+                  fold(acc);
+                } else {
 #pragma unroll
-                for (int c = 0; c < CT; ++c) {
-                  qp[c] = fma(acc[c][0], acc[c][0], qp[c]);
-                  qp[c] = fma(acc[c][1], acc[c][1], qp[c]);
-                  qp[c] = fma(acc[c][2], acc[c][2], qp[c]);
-                  qp[c] = fma(acc[c][3], acc[c][3], qp[c]);
-                  // pin the fold here: sunk to the softmax, every row tile would keep its own accumulators
-                  asm volatile("" : "+v"(qp[c]));
-                  acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
+                  for (int c = 0; c < CT; ++c) accp[c] = acc[c];
                 }
+#pragma unroll
+                for (int c = 0; c < CT; ++c) acc[c] = f64x4{0.0, 0.0, 0.0, 0.0};
               }
             }
             // after the last GL block: log-probability and the online softmax (FP64)
             if constexpr (b == G::GL_BLOCKS - 1) {
+              F64_STAMP(0);
               double lp[CT];
               bool need = false;
 #pragma unroll
@@ -341,9 +440,11 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
                 p[c] = (lp[c] == QCE_NEG_INF) ? 0.0 : exp(lp[c] - m[c]);
                 ssum[c] += p[c];
               }
+              F64_STAMP(1);
             }
           },
           std::make_integer_sequence<int, G::BPC>{});
+      F64_STAMP(2);
       cstream += G::CPC;
     }
 
@@ -394,6 +495,8 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
       }
     }
   }
+  F64_STAMP(5);
+  F64_STAMP_FLUSH
   wait_vmcnt<0>();  // drain the (dummy) ring prefetches before the workgroup retires
 }
 
@@ -404,9 +507,19 @@ constexpr int qce_f64_ct(int MP, int NP) { return (MP <= 64 && NP <= 64) ? 2 : 1
 
 template <int MP, int NP, bool HM, bool OP>
 hipError_t qce_f64_launch_t(const QceF64Args& a, hipStream_t st) {
-  constexpr int CT = qce_f64_ct(MP, NP), NW = 4;
+  constexpr int CT0 = qce_f64_ct(MP, NP);
+  if constexpr (CT0 == 2) {
+    if (a.waves == 8) {  // two waves per SIMD, one column tile each (same tile of 128 samples)
+      hipLaunchKernelGGL((k_est_all_f64<MP, NP, HM, 1, 8, OP>), dim3((unsigned)a.nwg), dim3(8 * 64), 0, st, a.B, a.M,
+                         a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa, a.pk,
+                         a.shift, a.stamps);
+      return hipGetLastError();
+    }
+  }
+  constexpr int CT = CT0, NW = 4;
   hipLaunchKernelGGL((k_est_all_f64<MP, NP, HM, CT, NW, OP>), dim3((unsigned)a.nwg), dim3(NW * 64), 0, st, a.B, a.M,
-                     a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa, a.pk, a.shift);
+                     a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa, a.pk, a.shift,
+                     a.stamps);
   return hipGetLastError();
 }
 

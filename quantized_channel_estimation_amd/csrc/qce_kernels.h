@@ -100,6 +100,8 @@ struct QceF64Args {
   double *pm, *ps, *pa;  // scratch for cut tiles: nwg * 2 * tile records
   double* pk = nullptr;   // shifted packed partial B x (2N+2): [s e^{m-shift}, 0, acc e^{m-shift}] (instead of om/os/oa)
   double shift = 0.0;
+  unsigned long long* stamps = nullptr;  // diagnostic builds (-DQCE_STAMPS): per-wave segment cycles
+  int waves = 8;  // workgroup shape where M, N <= 64: 8 waves x 1 column tile (two per SIMD), or 4 x 2 (QCE_F64_WAVES=4)
 };
 bool qce_f64_shape(int MP, int NP);
 int qce_f64_tile(int MP, int NP);  // samples per workgroup tile
