@@ -27,6 +27,7 @@ _vp = ctypes.c_void_p
 # name -> (restype, argtypes); every symbol include/qce.h declares
 SIGNATURES = {
     "qce_version": (ctypes.c_int, []),
+    "qce_build_id": (ctypes.c_char_p, []),
     "qce_last_error": (ctypes.c_char_p, []),
     "qce_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "qce_model_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, ctypes.c_int,
@@ -110,6 +111,21 @@ def check(rc):
     if rc == QCE_ENOTIMPL:
         raise NotImplementedError(msg)
     raise QceError(f"[qce status {rc}] {msg}")
+
+
+def build_id():
+    """Source digest the loaded libqce.so was built from (qce_build_id)."""
+    return load().qce_build_id().decode()
+
+
+def check_build_current():
+    """Raise if the loaded library was not built from the sources in this tree (a stale libqce.so)."""
+    from . import build as _b
+    if not os.path.isdir(_b.CSRC):
+        return
+    want, have = _b.source_digest(), build_id()
+    if have.split("-")[0] != want:
+        raise QceError(f"{LIB_PATH} was built from sources {have}, the tree has {want}: rebuild it")
 
 
 def device_count():

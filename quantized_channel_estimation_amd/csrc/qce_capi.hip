@@ -452,7 +452,7 @@ int check_model(qce_model* m, bool need_prepared) {
 
 extern "C" {
 
-int qce_version(void) { return 100; }
+int qce_version(void) { return 200; }
 
 const char* qce_last_error(void) { return g_err.c_str(); }
 

@@ -45,3 +45,12 @@ def test_no_device_is_a_loud_error():
         pytest.skip("a GPU is visible")
     with pytest.raises(RuntimeError):
         _lib.DeviceModel(np.zeros((2, 4), complex), np.stack([np.eye(4, dtype=complex)] * 2), np.array([0.5, 0.5]))
+
+
+def test_library_build_id_is_this_tree():
+    """qce_build_id() of the library the package loads is the digest of the csrc/ it sits next to
+    (smoke() asserts the same on the GPU box), so a stale prebuilt .so cannot pass for HEAD's."""
+    from quantized_channel_estimation_amd import build, _lib
+    build.build()
+    assert _lib.build_id() == build.source_digest()
+    _lib.check_build_current()

@@ -2,7 +2,9 @@
 import numpy as np
 import pytest
 
-from conftest import MODELS, MODES, case_args, rel_fro
+import os
+
+from conftest import MODELS, MODES, ROOT, case_args, rel_fro
 from oracle import qce_oracle as O
 
 
@@ -81,3 +83,14 @@ def test_oracle_gain_kats():
         assert O.standard_step(nb) == q[f"delta_{nb}"]
     np.testing.assert_array_equal(O.quant(q["quant_in"], 1), q["quant_1"])
     np.testing.assert_array_equal(O.quant(q["quant_in"], 3, q["lloyd_3_5_thr"], q["lloyd_3_5_lab"]), q["quant_lloyd_3_5"])
+
+
+def test_cpu_baseline_timing_recorded():
+    """the loop-faithful oracle bench.py times as the CPU baseline runs within +-15% of the
+    reference's own estimate_from_y (and gives identical results) — measured in the build container by
+    tests/golden/time_reference.py, recorded in timing_ratio.json."""
+    import json
+    d = json.load(open(os.path.join(ROOT, "tests", "golden", "timing_ratio.json")))
+    for cfg in ("cfg1", "cfg2"):
+        assert 0.85 <= d[cfg]["ratio"] <= 1.15, (cfg, d[cfg]["ratio"])
+        assert d[cfg]["rel_fro"] < 1e-12
