@@ -111,11 +111,16 @@ int qce_estimate_partial_f64(qce_model* model, const double* y, int64_t B, doubl
 
 /* The K-shard partial scaled to a shift shared by all shards and packed for one SUM collective:
  * packed_out (B, 2N+2) f64, row b = [s_b e^{m_b - shift}, 0, acc_b e^{m_b - shift} (2N interleaved)].
- * With shift = max over ALL components of cconst (>= every lp, the quad form is >= 0) the element-wise sum
- * over shards of these rows gives h_b = acc / s exactly (rows whose sum underflows to s = 0 need the
- * two-step combine of the unshifted partials). */
-int qce_estimate_partial_shifted(qce_model* model, const double* y, int64_t B, double shift, double* packed_out, int io,
-                                 void* stream);
+ * shift: one double where `io` says (device memory for QCE_IO_DEVICE, so the shift can come from a device-side
+ * collective without a host round trip).  With shift = max over ALL components of cconst (>= every lp, the quad
+ * form is >= 0) the element-wise sum over shards of these rows gives h_b = acc / s exactly (rows whose sum
+ * underflows to s = 0 need the two-step combine of the unshifted partials). */
+int qce_estimate_partial_shifted(qce_model* model, const double* y, int64_t B, const double* shift, double* packed_out,
+                                 int io, void* stream);
+
+/* out[0] = max_k cconst_k of the last prepare (this shard's part of the shift above; the caller reduces it over
+ * shards with a MAX collective).  `out` where `io` says; device I/O is asynchronous on `stream`. */
+int qce_cconst_max(qce_model* model, double* out, int io, void* stream);
 
 /* Per-SNR tables for state mirroring (the reference mutates gm.means_, gm.covariances_,
  * gm.precisions_cholesky_, :262-313) and tests.  Host pointers, any may be NULL:

@@ -52,8 +52,8 @@ SIGNATURES = {
     "qce_log_prob": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int, _vp]),
     "qce_estimate_partial": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int, _vp]),
     "qce_estimate_partial_f64": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int, _vp]),
-    "qce_estimate_partial_shifted": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_double, _vp, ctypes.c_int,
-                                                    _vp]),
+    "qce_estimate_partial_shifted": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, _vp, _vp, ctypes.c_int, _vp]),
+    "qce_cconst_max": (ctypes.c_int, [_vp, _vp, ctypes.c_int, _vp]),
     "qce_get_tables": (ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "qce_model_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                       ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
@@ -290,18 +290,33 @@ class DeviceModel:
 
     def partial_shifted(self, y, shift, out=None, stream=None):
         """Shifted packed K-shard partial (qce_estimate_partial_shifted): (B, 2N+2) f64 rows
-        [s e^{m-shift}, 0, acc e^{m-shift}] that sum over shards."""
+        [s e^{m-shift}, 0, acc e^{m-shift}] that sum over shards.  shift: a float (host I/O) or a one-element
+        float64 tensor on the device (device I/O, no host round trip)."""
         io = IO_HOST if isinstance(y, np.ndarray) else IO_DEVICE
         B = y.shape[0]
         if io == IO_HOST:
             y = np.ascontiguousarray(y, dtype=np.complex128)
             out = np.empty((B, 2 * self.N + 2)) if out is None else out
-        elif out is None:
+            sh = np.array([float(shift)])
+        else:
             import torch
-            out = torch.empty((B, 2 * self.N + 2), dtype=torch.float64, device=y.device)
+            if out is None:
+                out = torch.empty((B, 2 * self.N + 2), dtype=torch.float64, device=y.device)
+            sh = shift if isinstance(shift, torch.Tensor) else torch.tensor([float(shift)], dtype=torch.float64,
+                                                                             device=y.device)
         self._order_before(y, io, stream)
-        check(load().qce_estimate_partial_shifted(self._h, ptr(y), int(B), float(shift), ptr(out), io, stream))
+        check(load().qce_estimate_partial_shifted(self._h, ptr(y), int(B), ptr(sh), ptr(out), io, stream))
         self._order_after(io, stream)
+        return out
+
+    def cconst_max(self, out=None, stream=None):
+        """max_k c_k of the last prepare: a float, or written into the one-element device tensor `out`
+        (asynchronously on `stream`)."""
+        if out is None:
+            v = np.empty(1)
+            check(load().qce_cconst_max(self._h, ptr(v), IO_HOST, None))
+            return float(v[0])
+        check(load().qce_cconst_max(self._h, ptr(out), IO_DEVICE, stream))
         return out
 
     def cconst(self):

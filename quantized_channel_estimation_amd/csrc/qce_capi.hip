@@ -77,6 +77,9 @@ struct qce_model {
   DevBuf<double2> A, Cy, Cr, Lw, Linv, Aeff, work, V, W, means_y, q0, bvec;
   DevBuf<double> gain, cconst, thr, lab;
   DevBuf<int> status;
+  int* status_host = nullptr;  // pinned copy of the last prepare's Cholesky status (read lazily)
+  hipEvent_t status_ev = nullptr;
+  int status_pending = 0;
   DevBuf<float> pack32;
   DevBuf<double> pack64;
   long long stride32 = 0, stride64 = 0;
@@ -100,6 +103,7 @@ struct qce_model {
   DevBuf<double> part_a64;  // FP64 partial accumulator behind the f32 qce_estimate_partial
   DevBuf<double> fp_pack;   // host-I/O staging of qce_estimate_partial_shifted
   DevBuf<double> w64_scr;   // FP64 selection weights (selective modes)
+  DevBuf<double> shift_scr;  // one double: staged K-shard shift / cconst max
   DevBuf<double2> WT;       // transposed filters W_k^T for the FP64 selective-mode kernel (built lazily)
   int wt_valid = 0;
   int cu_count = 256;
@@ -195,7 +199,7 @@ bool want_f64(const qce_model* m) {
 // per CU, the remaining tiles' (tile, component) items dealt out stream-K; final h, or the FP64
 // (m, s, acc) partial when h == nullptr (K-shard path)
 int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, double* oa,
-            hipStream_t st, double* pk = nullptr, double shift = 0.0) {
+            hipStream_t st, double* pk = nullptr, const double* shift = nullptr) {
   const long long TS = qce_f64_tile(m->MP, m->NP);
   const long long tiles = (B + TS - 1) / TS;
   long long slots = m->cu_count;  // 128 KB of LDS: one workgroup per CU
@@ -442,8 +446,47 @@ bool fft_mfma_enabled() {
   return !(e && strcmp(e, "lds") == 0);
 }
 
+// The Cholesky status of a prepare is copied to pinned host memory behind the prepare's kernels and read only
+// when a call synchronises anyway (host I/O, qce_synchronize, qce_get_tables): a prepare costs no host round
+// trip.  A failed prepare surfaces as QCE_ECHOL there (device-I/O estimates in between compute on NaN tables).
+int post_status(qce_model* m, hipStream_t st) {
+  const int K = m->K;
+  if (!m->status_host) {
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&m->status_host), sizeof(int) * K, hipHostMallocDefault));
+    HIPCHK(hipEventCreateWithFlags(&m->status_ev, hipEventDisableTiming));
+  }
+  HIPCHK(hipMemcpyAsync(m->status_host, m->status.p, sizeof(int) * K, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipEventRecord(m->status_ev, st));
+  m->status_pending = 1;
+  return QCE_OK;
+}
+
+int check_status(qce_model* m, bool block) {
+  if (!m->status_pending) return QCE_OK;
+  if (!block && hipEventQuery(m->status_ev) == hipErrorNotReady) return QCE_OK;
+  HIPCHK(hipEventSynchronize(m->status_ev));
+  m->status_pending = 0;
+  for (int k = 0; k < m->K; ++k)
+    if (m->status_host[k]) {
+      m->prepared = 0;
+      return fail(QCE_ECHOL,
+                  "Fitting the mixture model failed because some components have ill-defined empirical covariance "
+                  "(for instance caused by singleton or collapsed samples). Try to decrease the number of "
+                  "components, or increase reg_covar.");
+    }
+  return QCE_OK;
+}
+
+#define HOST_SYNC_CHECK(m, st)                      \
+  do {                                              \
+    HIPCHK(hipStreamSynchronize(st));               \
+    if (int rc_ = check_status((m), true)) return rc_; \
+  } while (0)
+
 int check_model(qce_model* m, bool need_prepared) {
   if (!m) return fail(QCE_EARG, "null model");
+  if (need_prepared && m->prepared)
+    if (int rc = check_status(m, false)) return rc;  // a failure already known surfaces at once
   if (need_prepared && !m->prepared) return fail(QCE_ESTATE, "qce_prepare has not been called on this model");
   return QCE_OK;
 }
@@ -552,6 +595,8 @@ int qce_model_destroy(qce_model* m) {
                   &m->m_scr, &m->s_scr})
     b->release();
   m->status.release();
+  if (m->status_host) (void)hipHostFree(m->status_host);
+  if (m->status_ev) (void)hipEventDestroy(m->status_ev);
   m->pack32.release();
   m->w_scr.release();
   m->acc_scr.release();
@@ -563,7 +608,8 @@ int qce_model_destroy(qce_model* m) {
   m->sp_a.release();
   m->yflag.release();
   m->pack_f64.release();
-  for (auto* b : {&m->fp_m, &m->fp_s, &m->fp_a, &m->part_a64, &m->fp_pack, &m->w64_scr}) b->release();
+  for (auto* b : {&m->fp_m, &m->fp_s, &m->fp_a, &m->part_a64, &m->fp_pack, &m->w64_scr, &m->shift_scr})
+    b->release();
   m->WT.release();
   for (auto* b : {&m->f_ceig, &m->f_rinvT, &m->f_cprime, &m->f_wT, &m->f_gain}) b->release();
   for (auto* b : {&m->f_col0, &m->f_mspec, &m->f_uT, &m->f_bT}) b->release();
@@ -708,20 +754,10 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
       HIPCHK(qce_launch_fft_pack(pa, m->f_rinvT.p, m->f_uT.p, m->f_cprime.p, m->f_wT.p, m->f_bT.p, st));
       m->fft_mfma = 1;
     }
-    std::vector<int> status(K);
-    HIPCHK(hipMemcpyAsync(status.data(), m->status.p, sizeof(int) * K, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    if ((rc = post_status(m, st))) return rc;
     m->M = N;
     m->fft_active = 1;
     m->dense_valid = 0;
-    for (int k = 0; k < K; ++k)
-      if (status[k]) {
-        m->prepared = 0;
-        return fail(QCE_ECHOL,
-                    "Fitting the mixture model failed because some components have ill-defined empirical covariance "
-                    "(for instance caused by singleton or collapsed samples). Try to decrease the number of "
-                    "components, or increase reg_covar.");
-      }
     m->prepared = 1;
     return QCE_OK;
   }
@@ -854,22 +890,12 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
     m->cstride16 = cs16;
     m->y_scale = y_scale;
   }
-  std::vector<int> status(K);
-  HIPCHK(hipMemcpyAsync(status.data(), m->status.p, sizeof(int) * K, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  if ((rc = post_status(m, st))) return rc;
   m->M = M;
   m->MP = MP;
   m->NP = NP;
   m->stride32 = s32;
   m->stride64 = s64;
-  for (int k = 0; k < K; ++k)
-    if (status[k]) {
-      m->prepared = 0;
-      return fail(QCE_ECHOL,
-                  "Fitting the mixture model failed because some components have ill-defined empirical covariance "
-                  "(for instance caused by singleton or collapsed samples). Try to decrease the number of "
-                  "components, or increase reg_covar.");
-    }
   m->prepared = 1;
   return QCE_OK;
 }
@@ -959,7 +985,7 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
   }
   if (io == QCE_IO_HOST) {
     HIPCHK(hipMemcpyAsync(h_out, dh, sizeof(double2) * (size_t)B * m->N, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HOST_SYNC_CHECK(m, st);
   }
   return QCE_OK;
 }
@@ -1005,7 +1031,7 @@ int qce_log_prob(qce_model* m, const double* X, int64_t B, double* lp_out, doubl
     if (lp_out) HIPCHK(hipMemcpyAsync(lp_out, dlp, sizeof(double) * BK, hipMemcpyDeviceToHost, st));
     if (proba_out) HIPCHK(hipMemcpyAsync(proba_out, dpr, sizeof(double) * BK, hipMemcpyDeviceToHost, st));
     if (labels_out) HIPCHK(hipMemcpyAsync(labels_out, dlab, sizeof(int64_t) * B, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HOST_SYNC_CHECK(m, st);
   }
   return QCE_OK;
 }
@@ -1052,7 +1078,7 @@ int qce_estimate_partial(qce_model* m, const double* y, int64_t B, double* m_out
     HIPCHK(hipMemcpyAsync(m_out, dm, sizeof(double) * B, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(s_out, ds, sizeof(double) * B, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(acc_out, da, sizeof(float) * (size_t)B * 2 * m->N, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HOST_SYNC_CHECK(m, st);
   }
   return QCE_OK;
 }
@@ -1089,16 +1115,16 @@ int qce_estimate_partial_f64(qce_model* m, const double* y, int64_t B, double* m
     HIPCHK(hipMemcpyAsync(m_out, dm, sizeof(double) * B, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(s_out, ds, sizeof(double) * B, hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(acc_out, da, sizeof(double) * (size_t)B * 2 * m->N, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HOST_SYNC_CHECK(m, st);
   }
   return QCE_OK;
 }
 
-int qce_estimate_partial_shifted(qce_model* m, const double* y, int64_t B, double shift, double* packed_out, int io,
-                                 void* stream) {
+int qce_estimate_partial_shifted(qce_model* m, const double* y, int64_t B, const double* shift, double* packed_out,
+                                 int io, void* stream) {
   int rc = check_model(m, true);
   if (rc) return rc;
-  if (B < 0 || (B > 0 && (!y || !packed_out))) return fail(QCE_EARG, "bad arguments");
+  if (B < 0 || (B > 0 && (!y || !packed_out || !shift))) return fail(QCE_EARG, "bad arguments");
   if (B == 0) return QCE_OK;
   DeviceGuard g(m->device);
   hipStream_t st = pick_stream(m, stream);
@@ -1106,12 +1132,16 @@ int qce_estimate_partial_shifted(qce_model* m, const double* y, int64_t B, doubl
   if ((rc = stage_input(m, y, B, io, st, &dy))) return rc;
   const size_t W = (size_t)B * (2 * m->N + 2);
   double* dp = packed_out;
+  const double* dshift = shift;
   if (io == QCE_IO_HOST) {
     HIPCHK(m->fp_pack.ensure(W));
     dp = m->fp_pack.p;
+    HIPCHK(m->shift_scr.ensure(1));
+    HIPCHK(hipMemcpyAsync(m->shift_scr.p, shift, sizeof(double), hipMemcpyHostToDevice, st));
+    dshift = m->shift_scr.p;
   }
   if (!m->fft_active && m->f64_active) {
-    if ((rc = run_f64(m, dy, B, nullptr, nullptr, nullptr, nullptr, st, dp, shift))) return rc;
+    if ((rc = run_f64(m, dy, B, nullptr, nullptr, nullptr, nullptr, st, dp, dshift))) return rc;
   } else {  // other paths: their (m, s, acc) partial, scaled and packed
     HIPCHK(m->m_scr.ensure((size_t)B));
     HIPCHK(m->s_scr.ensure((size_t)B));
@@ -1119,11 +1149,29 @@ int qce_estimate_partial_shifted(qce_model* m, const double* y, int64_t B, doubl
     if ((rc = qce_estimate_partial_f64(m, reinterpret_cast<const double*>(dy), B, m->m_scr.p, m->s_scr.p,
                                        m->part_a64.p, QCE_IO_DEVICE, st)))
       return rc;
-    HIPCHK(qce_launch_pack_shifted(B, m->N, m->m_scr.p, m->s_scr.p, m->part_a64.p, nullptr, shift, dp, st));
+    HIPCHK(qce_launch_pack_shifted(B, m->N, m->m_scr.p, m->s_scr.p, m->part_a64.p, nullptr, dshift, dp, st));
   }
   if (io == QCE_IO_HOST) {
     HIPCHK(hipMemcpyAsync(packed_out, dp, sizeof(double) * W, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
+    HOST_SYNC_CHECK(m, st);
+  }
+  return QCE_OK;
+}
+
+int qce_cconst_max(qce_model* m, double* out, int io, void* stream) {
+  int rc = check_model(m, true);
+  if (rc) return rc;
+  if (!out) return fail(QCE_EARG, "null out");
+  DeviceGuard g(m->device);
+  hipStream_t st = pick_stream(m, stream);
+  if (m->fft_active && (rc = ensure_dense(m))) return rc;
+  if (io == QCE_IO_HOST) {
+    HIPCHK(m->shift_scr.ensure(1));
+    HIPCHK(qce_launch_cconst_max(m->K, m->cconst.p, m->shift_scr.p, st));
+    HIPCHK(hipMemcpyAsync(out, m->shift_scr.p, sizeof(double), hipMemcpyDeviceToHost, st));
+    HOST_SYNC_CHECK(m, st);
+  } else {
+    HIPCHK(qce_launch_cconst_max(m->K, m->cconst.p, out, st));
   }
   return QCE_OK;
 }
@@ -1136,7 +1184,7 @@ int qce_get_tables(qce_model* m, double* means_y, double* Cy, double* Cr, double
   DeviceGuard g(m->device);
   hipStream_t st = m->stream;
   const int K = m->K, M = m->M, N = m->N;
-  HIPCHK(hipStreamSynchronize(st));
+  HOST_SYNC_CHECK(m, st);
   auto cp = [&](double* dst, const void* src, size_t bytes) -> hipError_t {
     if (!dst) return hipSuccess;
     return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
@@ -1336,7 +1384,7 @@ int qce_em_estep(qce_model* m, const double* X, int64_t B, double* resp_out, dou
       HIPCHK(hipMemcpyAsync(mean_lse_out, dmean, sizeof(double), hipMemcpyDeviceToHost, st));
     }
   }
-  if (io == QCE_IO_HOST) HIPCHK(hipStreamSynchronize(st));
+  if (io == QCE_IO_HOST) HOST_SYNC_CHECK(m, st);
   return QCE_OK;
 }
 
@@ -1478,7 +1526,7 @@ static int assigned_impl(qce_model* m, const double* y, int64_t B, const int64_t
     if (io == QCE_IO_HOST)
       HIPCHK(hipMemcpyAsync(h_out, dh, sizeof(double2) * (size_t)B * m->N, hipMemcpyDeviceToHost, st));
   }
-  if (io == QCE_IO_HOST) HIPCHK(hipStreamSynchronize(st));
+  if (io == QCE_IO_HOST) HOST_SYNC_CHECK(m, st);
   return QCE_OK;
 }
 
@@ -1659,7 +1707,7 @@ int qce_synchronize(qce_model* m) {
   if (!m) return fail(QCE_EARG, "null model");
   DeviceGuard g(m->device);
   HIPCHK(hipStreamSynchronize(m->stream));
-  return QCE_OK;
+  return check_status(m, true);
 }
 
 }  // extern "C"

@@ -8,7 +8,8 @@ __global__ __launch_bounds__(256) void k_merge_f64(long long B, int N, int K, in
                                                    const double* __restrict__ pm, const double* __restrict__ ps,
                                                    const double* __restrict__ pa, double2* __restrict__ h,
                                                    double* __restrict__ om, double* __restrict__ os,
-                                                   double* __restrict__ oa, double* __restrict__ pk, double shift) {
+                                                   double* __restrict__ oa, double* __restrict__ pk,
+                                                   const double* __restrict__ shift) {
   const long long b = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (b >= B || L <= 0) return;
@@ -26,7 +27,7 @@ __global__ __launch_bounds__(256) void k_merge_f64(long long B, int N, int K, in
     const long long r = rec_of(w);
     s += (pm[r] == QCE_NEG_INF) ? 0.0 : ps[r] * exp(pm[r] - mx);
   }
-  const double psc = (pk && mx != QCE_NEG_INF) ? exp(mx - shift) : 0.0;  // shifted packed output
+  const double psc = (pk && mx != QCE_NEG_INF) ? exp(mx - *shift) : 0.0;  // shifted packed output
   for (int n = lane; n < N; n += 64) {
     double re = 0.0, im = 0.0;
     for (long long w = wa; w <= wb; ++w) {
@@ -57,12 +58,12 @@ __global__ __launch_bounds__(256) void k_merge_f64(long long B, int N, int K, in
 // [m, s, acc] partial (acc f64, or f32 when acc32) -> shifted packed [s e^{m-M*}, 0, acc e^{m-M*}]
 __global__ __launch_bounds__(256) void k_pack_shifted(long long B, int N, const double* __restrict__ m,
                                                       const double* __restrict__ s, const double* __restrict__ acc,
-                                                      const float* __restrict__ acc32, double shift,
+                                                      const float* __restrict__ acc32, const double* __restrict__ shift,
                                                       double* __restrict__ pk) {
   const long long W = 2LL * N + 2;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < B * W; i += (long long)gridDim.x * 256) {
     const long long b = i / W, j = i % W;
-    const double sc = (m[b] == QCE_NEG_INF) ? 0.0 : exp(m[b] - shift);
+    const double sc = (m[b] == QCE_NEG_INF) ? 0.0 : exp(m[b] - *shift);
     double v;
     if (j == 0) v = s[b];
     else if (j == 1) v = 0.0;
@@ -71,7 +72,7 @@ __global__ __launch_bounds__(256) void k_pack_shifted(long long B, int N, const 
   }
 }
 hipError_t qce_launch_pack_shifted(long long B, int N, const double* m, const double* s, const double* acc,
-                                   const float* acc32, double shift, double* pk, hipStream_t st) {
+                                   const float* acc32, const double* shift, double* pk, hipStream_t st) {
   long long blocks = (B * (2LL * N + 2) + 255) / 256;
   blocks = blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks);
   hipLaunchKernelGGL(k_pack_shifted, dim3((unsigned)blocks), dim3(256), 0, st, B, N, m, s, acc, acc32, shift, pk);
@@ -192,5 +193,22 @@ hipError_t qce_launch_f32_to_f64(const float* a, double* b, long long n, hipStre
   long long blocks = (n + 255) / 256;
   blocks = blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks);
   hipLaunchKernelGGL(k_f32_to_f64, dim3((unsigned)blocks), dim3(256), 0, st, a, b, n);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_cconst_max(int K, const double* __restrict__ c, double* __restrict__ out) {
+  __shared__ double red[256];
+  double v = -__builtin_inf();
+  for (int k = threadIdx.x; k < K; k += 256) v = fmax(v, c[k]);
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+hipError_t qce_launch_cconst_max(int K, const double* cconst, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_cconst_max, dim3(1), dim3(256), 0, st, K, cconst, out);
   return hipGetLastError();
 }

@@ -172,7 +172,7 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
                                                          double* __restrict__ om, double* __restrict__ os,
                                                          double* __restrict__ oa, double* __restrict__ pm,
                                                          double* __restrict__ ps, double* __restrict__ pa,
-                                                         double* __restrict__ pk, double shift,
+                                                         double* __restrict__ pk, const double* __restrict__ shift,
                                                          unsigned long long* __restrict__ stamps) {
   using G = F64G<MP, NP, HM>;
   constexpr int TS = NW * 16 * CT;           // samples per tile
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
       const bool pfmt = OUT_PARTIAL || !whole;
       const long long row = whole ? sample : (w * 2 + (t == t_first ? 0 : 1)) * TS + ls;
       if (OUT_PARTIAL && whole && pk) {  // shifted packed partial: [s e^{m-M*}, 0, acc e^{m-M*}] (K-shard sum)
-        const double sc = (m[c] == QCE_NEG_INF) ? 0.0 : exp(m[c] - shift);
+        const double sc = (m[c] == QCE_NEG_INF) ? 0.0 : exp(m[c] - *shift);
         double* dp = pk + sample * (2LL * N + 2);
         if (g == 0) *reinterpret_cast<double2*>(dp) = make_double2(ssum[c] * sc, 0.0);
 #pragma unroll

@@ -99,7 +99,7 @@ struct QceF64Args {
   double *om, *os, *oa;  // partial-format output (K-shard path), oa B x 2N
   double *pm, *ps, *pa;  // scratch for cut tiles: nwg * 2 * tile records
   double* pk = nullptr;   // shifted packed partial B x (2N+2): [s e^{m-shift}, 0, acc e^{m-shift}] (instead of om/os/oa)
-  double shift = 0.0;
+  const double* shift = nullptr;  // device pointer: the shared shift M* of the packed partial
   unsigned long long* stamps = nullptr;  // diagnostic builds (-DQCE_STAMPS): per-wave segment cycles
   int waves = 8;  // workgroup shape where M, N <= 64: 8 waves x 1 column tile (two per SIMD), or 4 x 2 (QCE_F64_WAVES=4)
 };
@@ -111,7 +111,9 @@ hipError_t qce_launch_pack_f64all(int K, int M, int N, int MP, int NP, int has_m
                                   hipStream_t st);
 hipError_t qce_launch_est_f64(const QceF64Args& a, bool out_partial, hipStream_t st);
 hipError_t qce_launch_pack_shifted(long long B, int N, const double* m, const double* s, const double* acc,
-                                   const float* acc32, double shift, double* pk, hipStream_t st);
+                                   const float* acc32, const double* shift, double* pk, hipStream_t st);
+// out[0] = max_k cconst[k] (device), the local part of the K-shard shift M*
+hipError_t qce_launch_cconst_max(int K, const double* cconst, double* out, hipStream_t st);
 hipError_t qce_launch_f64_to_f32(const double* a, float* b, long long n, hipStream_t st);
 hipError_t qce_launch_f32_to_f64(const float* a, double* b, long long n, hipStream_t st);
 

@@ -120,6 +120,18 @@ __global__ void k_cy_identity(int N, long long total, const double2* __restrict_
   Cy[idx] = v;
 }
 
+// X_k = Linv_k diag(g_k) (M x M): the Linv Aeff product when A = I
+__global__ void k_scale_cols(int M, long long total, const double2* __restrict__ Linv, const double* __restrict__ g,
+                             double2* __restrict__ X) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const long long k = idx / ((long long)M * M);
+  const int j = (int)(idx % M);
+  const double gj = g[k * M + j];
+  const double2 v = Linv[idx];
+  X[idx] = make_double2(v.x * gj, v.y * gj);
+}
+
 __global__ void k_diag_add(int M, int K, double2* __restrict__ Cy, double s2) {
   int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= K * M) return;
@@ -355,6 +367,168 @@ __global__ __launch_bounds__(256) void k_chol_inv_lds(int M, const double2* __re
   }
 }
 
+// Cholesky Cr_k = L L^H and L^{-1} for M <= 64 by ONE wave per component (lane r owns row r; the matrix in LDS
+// with a padded row stride, 66.5 KB), wave-synchronous: no multi-wave barriers in the 2M sequential steps, which
+// is what bounds a per-component factorisation (the K components run side by side, two per CU).
+//   factor   step j: a_rc -= (a_rj / a_jj) conj(a_cj) for r > j, every c > j (deferred scaling: L = A~ D^-1/2,
+//            D = diag a_jj).  Updating whole rows keeps the inner trip count uniform; the upper triangle it
+//            touches is never read.  conj(a_cj) is staged in its own LDS vector so the unrolled loop's loads
+//            and stores provably do not alias.
+//   inverse  Y = A~^{-1} by forward substitution (lane c owns column c; Y_kc = 0 for k < c is stored, so the
+//            inner sum runs over k < i in every lane), written over A~ row by row, then Linv = D^{1/2} Y.
+__global__ __launch_bounds__(64) void k_chol_inv_wave(int M, const double2* __restrict__ Cr, double2* __restrict__ Linv,
+                                                      const double* __restrict__ logw, double* __restrict__ cconst,
+                                                      int* __restrict__ status) {
+  constexpr int LD = 65;  // padded row stride (complex elements)
+  __shared__ double2 a[64 * LD];
+  __shared__ double2 v[64];
+  __shared__ double dg[64];
+  const int k = blockIdx.x, lane = threadIdx.x;
+  const double2* src = Cr + (long long)k * M * M;
+  for (int e = lane; e < M * M; e += 64) {
+    const int r = e / M, c = e % M;
+    a[r * LD + c] = src[e];
+  }
+  __syncthreads();
+  const int r = lane;
+  for (int j = 0; j < M; ++j) {
+    const double ajj = a[j * LD + j].x;  // final after step j - 1 (same value in every lane)
+    if (!(ajj > 0.0)) {
+      if (lane == 0) status[k] = 1;
+      return;
+    }
+    if (lane < M) {
+      const double2 x = a[lane * LD + j];
+      v[lane] = make_double2(x.x, -x.y);
+    }
+    __syncthreads();
+    if (r > j && r < M) {
+      const double2 arj = a[r * LD + j];
+      const double inv = 1.0 / ajj;
+      const double2 s2 = make_double2(arj.x * inv, arj.y * inv);
+      double2* row = a + r * LD;
+#pragma unroll 8
+      for (int c = j + 1; c < M; ++c) row[c] = csub(row[c], cmul(s2, v[c]));
+    }
+    __syncthreads();
+  }
+  if (lane < M) dg[lane] = a[lane * LD + lane].x;
+  __syncthreads();
+  const int c = lane;
+  for (int i = 0; i < M; ++i) {
+    double2 t = make_double2(c == i ? 1.0 : 0.0, 0.0);
+    if (c < M) {
+      const double2* ai = a + i * LD;
+#pragma unroll 8
+      for (int kk = 0; kk < i; ++kk) t = csub(t, cmul(ai[kk], a[kk * LD + c]));
+    }
+    __syncthreads();  // every read of row i done before it is overwritten
+    if (c < M) {
+      const double di = 1.0 / dg[i];
+      a[i * LD + c] = c <= i ? make_double2(t.x * di, t.y * di) : make_double2(0.0, 0.0);
+    }
+    __syncthreads();
+  }
+  double2* dst = Linv + (long long)k * M * M;
+  for (int e = lane; e < M * M; e += 64) {
+    const int i = e / M, cc = e % M;
+    const double sd = sqrt(dg[i]);
+    const double2 y = a[i * LD + cc];
+    dst[e] = make_double2(y.x * sd, y.y * sd);
+  }
+  if (lane == 0) {
+    double ld = 0.0;
+    for (int i = 0; i < M; ++i) ld += log(1.0 / sqrt(dg[i]));
+    cconst[k] = -(M * log(3.14159265358979323846)) + 2.0 * ld + logw[k];
+    status[k] = 0;
+  }
+}
+
+// Cholesky Cr_k = L L^H and L^{-1} for M <= MM (64 or 128) with the lower triangle packed in LDS (row-major,
+// idx(i, j) = i(i+1)/2 + j; 128 -> 132 KB), one workgroup per component, 256 threads = 64 groups of 4 lanes,
+// a group owning a row (its 4 lanes split the columns):
+//   factor   step j (one barrier): a_rc -= a_rj conj(a_cj) / a_jj for j < c <= r   (deferred scaling as in
+//            k_chol_inv_lds); afterwards L_ij = a_ij / sqrt(a_jj)
+//   inverse  in place, LAPACK trti2 order (j = M-1 .. 0): X_jj = 1 / L_jj, X_ij = -X_jj sum_{k=j+1..i} X_ik L_kj
+//            for i > j (the trailing block is already inverted); row sums of a group reduced by lane shuffles,
+//            the new column staged in LDS (two barriers per step)
+// Status and c_k as k_chol_inv (gmm_cplx_bussgang.py:15-82: LinAlgError -> ValueError in the caller).
+template <int MM>
+__global__ __launch_bounds__(256) void k_chol_inv_tri(int M, const double2* __restrict__ Cr, double2* __restrict__ Linv,
+                                                      const double* __restrict__ logw, double* __restrict__ cconst,
+                                                      int* __restrict__ status) {
+  __shared__ double2 a[MM * (MM + 1) / 2];
+  __shared__ double2 col[MM];
+  __shared__ double piv[MM];
+  const int k = blockIdx.x, tid = threadIdx.x, grp = tid >> 2, sub = tid & 3;
+  auto idx = [](int i, int j) { return i * (i + 1) / 2 + j; };
+  const double2* src = Cr + (long long)k * M * M;
+  for (int e = tid; e < M * M; e += 256) {
+    const int r = e / M, c = e % M;
+    if (c <= r) a[idx(r, c)] = src[e];
+  }
+  __syncthreads();
+  // ---- factor ----
+  for (int j = 0; j < M; ++j) {
+    const double ajj = a[idx(j, j)].x;  // final: updated by step j - 1 before the barrier
+    if (!(ajj > 0.0)) {                 // same value in every thread: uniform exit
+      if (tid == 0) status[k] = 1;
+      return;
+    }
+    const double inv = 1.0 / ajj;
+    for (int r = j + 1 + grp; r < M; r += 64) {
+      const double2 arj = a[idx(r, j)];
+      const double2 s2 = make_double2(arj.x * inv, arj.y * inv);
+      const int base = idx(r, 0);
+      for (int c = j + 1 + sub; c <= r; c += 4) {
+        const double2 acj = a[idx(c, j)];
+        a[base + c] = csub(a[base + c], cmulc(s2, acj));
+      }
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < M; i += 256) piv[i] = sqrt(a[idx(i, i)].x);
+  __syncthreads();
+  for (int e = tid; e < M * (M + 1) / 2; e += 256) {  // L_ij = a_ij / sqrt(a_jj)
+    int r = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+    if ((r + 1) * (r + 2) / 2 <= e) ++r;
+    if (r * (r + 1) / 2 > e) --r;
+    const int c = e - r * (r + 1) / 2;
+    const double2 v = a[e];
+    a[e] = make_double2(v.x / piv[c], v.y / piv[c]);
+  }
+  __syncthreads();
+  // ---- in-place inverse ----
+  for (int j = M - 1; j >= 0; --j) {
+    const double xjj = 1.0 / a[idx(j, j)].x;  // real positive diagonal
+    for (int i = j + 1 + grp; i < M; i += 64) {  // the 4 lanes of a group share the trip count (shuffle partners)
+      double2 t = make_double2(0.0, 0.0);
+      const int base = idx(i, 0);
+      for (int kk = j + 1 + sub; kk <= i; kk += 4) t = cfma(a[base + kk], a[idx(kk, j)], t);
+      t.x += __shfl_xor(t.x, 1);
+      t.y += __shfl_xor(t.y, 1);
+      t.x += __shfl_xor(t.x, 2);
+      t.y += __shfl_xor(t.y, 2);
+      if (sub == 0) col[i] = make_double2(-xjj * t.x, -xjj * t.y);
+    }
+    __syncthreads();
+    for (int i = j + 1 + tid; i < M; i += 256) a[idx(i, j)] = col[i];
+    if (tid == 0) a[idx(j, j)] = make_double2(xjj, 0.0);
+    __syncthreads();
+  }
+  double2* dst = Linv + (long long)k * M * M;
+  for (int e = tid; e < M * M; e += 256) {
+    const int r = e / M, c = e % M;
+    dst[e] = c <= r ? a[idx(r, c)] : make_double2(0.0, 0.0);
+  }
+  if (tid == 0) {
+    double ld = 0.0;
+    for (int i = 0; i < M; ++i) ld += log(1.0 / piv[i]);
+    cconst[k] = -(M * log(3.14159265358979323846)) + 2.0 * ld + logw[k];
+    status[k] = 0;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Packing of the FP32 fused-kernel tables (32x32x2 MFMA A-operand order).
 // Real embedding with interleaved (re, im): E[2i][2j]=Re, E[2i][2j+1]=-Im, E[2i+1][2j]=Im, E[2i+1][2j+1]=Re.
@@ -500,7 +674,9 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
                      p.kind, p.n_bits, p.quant_kind, p.delta, p.thr, p.lab, p.beta_first);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (M <= 64) {
-    hipLaunchKernelGGL(k_chol_inv_lds, dim3(K), dim3(256), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
+    hipLaunchKernelGGL(k_chol_inv_wave, dim3(K), dim3(64), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
+  } else if (M <= 128) {
+    hipLaunchKernelGGL(k_chol_inv_tri<128>, dim3(K), dim3(256), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
   } else {
     if ((e = hipMemcpyAsync(p.Lw, p.Cr, sizeof(double2) * (size_t)K * M * M, hipMemcpyDeviceToDevice, st)) !=
         hipSuccess)
@@ -508,10 +684,16 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
     hipLaunchKernelGGL(k_chol_inv, dim3(K), dim3(256), 0, st, M, p.Lw, p.Linv, p.logw, p.cconst, p.status);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  // X = Linv Aeff (M x N) -> work
-  if ((e = zgemm(0, 0, M, N, M, one, p.Linv, M, (long long)M * M, p.Aeff, N, (long long)M * N, zero, p.work, N,
-                 (long long)M * N, K, st)) != hipSuccess)
+  // X = Linv Aeff (M x N) -> work; with A = I, Aeff = diag(gain): a column scaling of Linv
+  if (p.identityA) {
+    const long long total = (long long)K * M * M;
+    hipLaunchKernelGGL(k_scale_cols, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, M, total, p.Linv,
+                       p.gain, p.work);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  } else if ((e = zgemm(0, 0, M, N, M, one, p.Linv, M, (long long)M * M, p.Aeff, N, (long long)M * N, zero, p.work,
+                        N, (long long)M * N, K, st)) != hipSuccess) {
     return e;
+  }
   // V = C X^H (N x M)
   if ((e = zgemm(0, 2, N, M, N, one, p.covs, N, (long long)N * N, p.work, N, (long long)M * N, zero, p.V, M,
                  (long long)N * M, K, st)) != hipSuccess)

@@ -130,16 +130,20 @@ class ComponentShardEstimator:
         self._bufs = {}
 
     def prepare(self, A, snr_db, n_bits, quant_kind=_lib.QUANT_UNIFORM, thresholds=None, labels=None, stream=None):
-        """Per-rank prepare of its components and the common shift M* (one scalar MAX all-reduce)."""
+        """Per-rank prepare of its components and the common shift M* (one scalar MAX all-reduce).  On the GPU
+        the shift stays on the device: this rank's max c_k is written by a kernel on torch's current stream and
+        all-reduced there, and the partial kernels read it — no host round trip per SNR point."""
         import torch
         import torch.distributed as dist
-        self.dev.prepare(A, snr_db, n_bits, quant_kind, thresholds, labels, stream=stream)
-        c = self.dev.cconst()
-        dev = torch.device("cuda", self.dev.device) if torch.cuda.is_available() else torch.device("cpu")
-        t = torch.tensor([float(np.max(c))], dtype=torch.float64, device=dev)
+        dev = torch.device("cuda", self.dev.device)
+        cur = torch.cuda.current_stream(dev)
+        self.dev.prepare(A, snr_db, n_bits, quant_kind, thresholds, labels,
+                         stream=stream if stream is not None else cur.cuda_stream)
+        if not isinstance(self.shift, torch.Tensor):
+            self.shift = torch.empty(1, dtype=torch.float64, device=dev)
+        self.dev.cconst_max(out=self.shift, stream=cur.cuda_stream)
         if self.world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-        self.shift = float(t.item())
+            dist.all_reduce(self.shift, op=dist.ReduceOp.MAX, group=self.group)
 
     def _buf(self, key, shape, device):
         import torch
