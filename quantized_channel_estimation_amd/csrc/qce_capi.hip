@@ -437,6 +437,7 @@ QceFftEstArgs fft_args(qce_model* m, const double2* y, long long B) {
   a.pw = m->f_pw.p;
   a.pbr = m->f_pbr.p;
   a.pbi = m->f_pbi.p;
+  a.cu = m->cu_count;
   return a;
 }
 

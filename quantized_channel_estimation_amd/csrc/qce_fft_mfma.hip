@@ -44,13 +44,14 @@ QCE_DEV double2 rootmul(double2 v, int P, int mm) {
 // Forward (DIF): stage s pairs (m, m + R/2^{s+1}) with twiddle W_{2D_s}^{j + (m mod half) E}.
 // Inverse (DIT): the same stages in reverse order, conjugate twiddles.
 template <int RL, bool INV>
-QCE_DEV void fft_pass(double2* T, int lgTS, int RS, int lgN, int lgL, int st, int lgD, const double2* tw) {
+QCE_DEV void fft_pass(double2* T, int lgTS, int RS, int lgN, int lgL, int st, int lgD, const double2* tw, int t0,
+                      int nthr) {
   constexpr int R = 1 << RL;
   const int lgE = lgD + 1 - RL;
   const int lgnb = lgL - lgD - 1;  // blocks per line
   const int total = 1 << (lgTS + lgN - RL);
   const int TSm = (1 << lgTS) - 1;
-  for (int it = threadIdx.x; it < total; it += 256) {
+  for (int it = t0; it < total; it += nthr) {
     const int s = it & TSm, q = it >> lgTS;
     const int j = q & ((1 << lgE) - 1), rest = q >> lgE;
     const int blk = rest & ((1 << lgnb) - 1), line = rest >> lgnb;
@@ -100,8 +101,19 @@ QCE_DEV void fft_pass(double2* T, int lgTS, int RS, int lgN, int lgL, int st, in
   }
 }
 
-template <bool INV>
+// Orders one wave's LDS accesses without a workgroup barrier: a wave's LDS instructions complete in
+// issue order, so a compiler fence around the wave barrier is all the wave-local FFT passes need.
+QCE_DEV void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// WAVE: the passes run over one wave's own tile (64 lanes, wave-local ordering); otherwise over the
+// workgroup's tile (256 threads, __syncthreads between passes)
+template <bool INV, bool WAVE = false>
 QCE_DEV void fft_axis_passes(double2* T, int lgTS, int RS, int lgN, int lgL, int st, const double2* tw) {
+  const int t0 = WAVE ? (int)(threadIdx.x & 63) : (int)threadIdx.x, nthr = WAVE ? 64 : 256;
   // forward: half-distances L/2 .. 1 in groups of <= 3 stages; inverse: the same passes reversed
   int rl[3], dd[3], np = 0;
   for (int rem = lgL, lgD = lgL - 1; rem > 0;) {
@@ -114,10 +126,11 @@ QCE_DEV void fft_axis_passes(double2* T, int lgTS, int RS, int lgN, int lgL, int
   }
   for (int i = 0; i < np; ++i) {
     const int p = INV ? np - 1 - i : i;
-    if (rl[p] == 3) fft_pass<3, INV>(T, lgTS, RS, lgN, lgL, st, dd[p], tw);
-    else if (rl[p] == 2) fft_pass<2, INV>(T, lgTS, RS, lgN, lgL, st, dd[p], tw);
-    else fft_pass<1, INV>(T, lgTS, RS, lgN, lgL, st, dd[p], tw);
-    __syncthreads();
+    if (rl[p] == 3) fft_pass<3, INV>(T, lgTS, RS, lgN, lgL, st, dd[p], tw, t0, nthr);
+    else if (rl[p] == 2) fft_pass<2, INV>(T, lgTS, RS, lgN, lgL, st, dd[p], tw, t0, nthr);
+    else fft_pass<1, INV>(T, lgTS, RS, lgN, lgL, st, dd[p], tw, t0, nthr);
+    if (WAVE) wave_lds_sync();
+    else __syncthreads();
   }
 }
 
@@ -294,8 +307,200 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
   for (int e = tid; e < rows * N; e += 256) ht[e] = T[(e >> lgN) * RS + (e & (N - 1))];
 }
 
+// N <= 64: one wave owns 16 observations end to end (load, FFT, both products, IFFT, store) with no
+// workgroup barrier after the twiddle table; waves loop over 16-observation tiles (persistent grid of
+// two workgroups per CU, 8 waves per CU).  The spectra stay in the wave's LDS tile through the component
+// loop, |Y|^2 in registers.  Tables are in fragment order (k_fft_pack): a lane's operands for two
+// consecutive MFMAs are one 16-byte load, and block cb+1's operands are fetched while block cb computes.
+//   lp  table: [cb][t/2][lane][t&1] = -rinv[bin 4t + lane/16][comp 16cb + lane%16]       t < N/4
+//   filter   : [cb][j/2][lane][j&1] = w[comp 16cb + lane/16 + 4r][bin 16t + lane%16]     j = r NT + t
+template <int N, int OUT, bool HM>
+__global__ __launch_bounds__(256, 2) void k_fft_wave(long long B, long long ntiles, int lg1, int lg2, int Kp,
+                                                     const double2* __restrict__ y, const double* __restrict__ pr,
+                                                     const double* __restrict__ pur, const double* __restrict__ pui,
+                                                     const double* __restrict__ pc, const double* __restrict__ pw,
+                                                     const double* __restrict__ pbr, const double* __restrict__ pbi,
+                                                     double2* __restrict__ h, double* __restrict__ om,
+                                                     double* __restrict__ os, float* __restrict__ oa) {
+  constexpr int NT = N / 16;  // 16-bin tiles of the filter product
+  constexpr int NK = N / 4;   // k-steps of the lp product
+  constexpr int NL = NK / 2;  // 16-byte lp operand loads per block
+  constexpr int NW = 2 * NT;  // 16-byte filter operand loads per block
+  constexpr int RS = N + 1;
+  constexpr int lgN = __builtin_ctz(N);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double2* tw = reinterpret_cast<double2*>(smem);
+  const int tid = threadIdx.x;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  double2* T = tw + 128 + wid * (16 * RS);
+  for (int t = tid; t < 128; t += 256) {
+    double sn, cs;
+    sincospi(-(double)t / 128.0, &sn, &cs);
+    tw[t] = make_double2(cs, sn);
+  }
+  __syncthreads();
+  const int col = lane & 15, hq = lane >> 4;
+  double2* Trow = T + col * RS;
+  const int ncb = Kp >> 4;
+  const double2* PR = reinterpret_cast<const double2*>(pr) + lane;
+  const double2* PW = reinterpret_cast<const double2*>(pw) + lane;
+  for (long long tile = (long long)blockIdx.x * 4 + wid; tile < ntiles; tile += (long long)gridDim.x * 4) {
+    const long long b0 = tile * 16;
+    const int rows = (int)((B - b0) < 16 ? (B - b0) : 16);
+    {
+      const double2* yt = y + b0 * N;
+#pragma unroll
+      for (int i = 0; i < N / 4; ++i) {
+        const int e = lane + 64 * i, r = e >> lgN;
+        T[r * RS + (e & (N - 1))] = (r < rows) ? yt[e] : make_double2(0.0, 0.0);
+      }
+    }
+    wave_lds_sync();
+    fft_axis_passes<false, true>(T, 4, RS, lgN, lg2, 1, tw);
+    if (lg1 > 0) fft_axis_passes<false, true>(T, 4, RS, lgN, lg1, 1 << lg2, tw);
+    double y2[NK];
+#pragma unroll
+    for (int t = 0; t < NK; ++t) {
+      const double2 v = Trow[4 * t + hq];
+      y2[t] = v.x * v.x + v.y * v.y;
+    }
+    f64x4 F[NT], Br[HM ? NT : 1], Bi[HM ? NT : 1];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      for (int r = 0; r < 4; ++r) F[t][r] = 0.0;
+    if constexpr (HM) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        for (int r = 0; r < 4; ++r) Br[t][r] = Bi[t][r] = 0.0;
+    }
+    double m = -__builtin_inf(), ssum = 0.0;
+    double2 ta[NL], tb[NW];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) ta[i] = PR[i * 64];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) tb[i] = PW[i * 64];
+    for (int cb = 0; cb < ncb; ++cb) {
+      const int c0 = cb << 4;
+      const int nb = (cb + 1 < ncb ? cb + 1 : cb);  // next block's operands (the last block re-reads its own)
+      double2 na[NL], nw[NW];
+#pragma unroll
+      for (int i = 0; i < NL; ++i) na[i] = PR[(nb * NL + i) * 64];
+#pragma unroll
+      for (int i = 0; i < NW; ++i) nw[i] = PW[(nb * NW + i) * 64];
+      f64x4 C;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) C[r] = pc[c0 + hq + 4 * r];
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        C = mfma16x16x4d(ta[i].x, y2[2 * i], C);
+        C = mfma16x16x4d(ta[i].y, y2[2 * i + 1], C);
+      }
+      if constexpr (HM) {
+        const double2* qa = reinterpret_cast<const double2*>(pur) + lane + cb * NL * 64;
+        const double2* qb = reinterpret_cast<const double2*>(pui) + lane + cb * NL * 64;
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+          const double2 ua = qa[i * 64], ub = qb[i * 64];
+          const double2 v0 = Trow[8 * i + hq], v1 = Trow[8 * i + 4 + hq];
+          C = mfma16x16x4d(ua.x, v0.x, C);
+          C = mfma16x16x4d(ub.x, v0.y, C);
+          C = mfma16x16x4d(ua.y, v1.x, C);
+          C = mfma16x16x4d(ub.y, v1.y, C);
+        }
+      }
+      // online softmax over this block of 16 components
+      double bm = fmax(fmax(C[0], C[1]), fmax(C[2], C[3]));
+      bm = fmax(bm, __shfl_xor(bm, 16));
+      bm = fmax(bm, __shfl_xor(bm, 32));
+      const double mn = fmax(m, bm);
+      double e[4], alpha = 1.0;
+      if (mn == -__builtin_inf()) {
+        e[0] = e[1] = e[2] = e[3] = 0.0;
+      } else {
+        alpha = exp(m - mn);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) e[r] = exp(C[r] - mn);
+      }
+      double ls = (e[0] + e[1]) + (e[2] + e[3]);
+      ls += __shfl_xor(ls, 16);
+      ls += __shfl_xor(ls, 32);
+      ssum = ssum * alpha + ls;
+      m = mn;
+#pragma unroll
+      for (int t = 0; t < NT; ++t) F[t] *= alpha;
+#pragma unroll
+      for (int j = 0; j < 4 * NT; ++j) {
+        const int r = j / NT, t = j % NT;
+        const double wv = (j & 1) ? tb[j >> 1].y : tb[j >> 1].x;
+        F[t] = mfma16x16x4d(wv, e[r], F[t]);
+      }
+      if constexpr (HM) {
+        const double2* qa = reinterpret_cast<const double2*>(pbr) + lane + cb * NW * 64;
+        const double2* qb = reinterpret_cast<const double2*>(pbi) + lane + cb * NW * 64;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          Br[t] *= alpha;
+          Bi[t] *= alpha;
+        }
+#pragma unroll
+        for (int j = 0; j < 4 * NT; ++j) {
+          const int r = j / NT, t = j % NT;
+          const double2 ua = qa[(j >> 1) * 64], ub = qb[(j >> 1) * 64];
+          Br[t] = mfma16x16x4d((j & 1) ? ua.y : ua.x, e[r], Br[t]);
+          Bi[t] = mfma16x16x4d((j & 1) ? ub.y : ub.x, e[r], Bi[t]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NL; ++i) ta[i] = na[i];
+#pragma unroll
+      for (int i = 0; i < NW; ++i) tb[i] = nw[i];
+    }
+    // Z = Y f + bb in place (each (observation, bin) of the tile belongs to exactly one lane)
+    const double sc = (OUT == 0) ? 1.0 / ssum : 1.0;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int bin = 16 * t + hq + 4 * r;
+        const double2 v = Trow[bin];
+        const double f = F[t][r] * sc;
+        if constexpr (HM)
+          Trow[bin] = make_double2(fma(v.x, f, Br[t][r] * sc), fma(v.y, f, Bi[t][r] * sc));
+        else
+          Trow[bin] = make_double2(v.x * f, v.y * f);
+      }
+    if (OUT == 3 && hq == 0 && col < rows) {
+      om[b0 + col] = m;
+      os[b0 + col] = ssum;
+    }
+    wave_lds_sync();
+    if (lg1 > 0) fft_axis_passes<true, true>(T, 4, RS, lgN, lg1, 1 << lg2, tw);
+    fft_axis_passes<true, true>(T, 4, RS, lgN, lg2, 1, tw);
+    if (OUT == 3) {
+      float2* at = reinterpret_cast<float2*>(oa) + b0 * N;
+#pragma unroll
+      for (int i = 0; i < N / 4; ++i) {
+        const int e = lane + 64 * i, r = e >> lgN;
+        if (r < rows) {
+          const double2 v = T[r * RS + (e & (N - 1))];
+          at[e] = make_float2((float)v.x, (float)v.y);
+        }
+      }
+    } else {
+      double2* ht = h + b0 * N;
+#pragma unroll
+      for (int i = 0; i < N / 4; ++i) {
+        const int e = lane + 64 * i, r = e >> lgN;
+        if (r < rows) ht[e] = T[r * RS + (e & (N - 1))];
+      }
+    }
+    wave_lds_sync();
+  }
+}
+
 // natural-order per-bin tables of k_fft_prep -> the kernel's storage order (bit-reversed per axis),
-// negated rinv, components padded to Kp (padding: c' = -inf, zero tables)
+// negated rinv, components padded to Kp (padding: c' = -inf, zero tables); N <= 64: fragment order of
+// k_fft_wave, otherwise the row-major N x Kp / Kp x N order of k_fft_mfma
 __global__ __launch_bounds__(256) void k_fft_pack(int N, int lg1, int lg2, int K, int Kp, int has_mean,
                                                   const double* __restrict__ rinvT, const double2* __restrict__ uT,
                                                   const double* __restrict__ cprime, const double* __restrict__ wT,
@@ -306,6 +511,39 @@ __global__ __launch_bounds__(256) void k_fft_pack(int N, int lg1, int lg2, int K
   const int n2m = (1 << lg2) - 1;
   auto bin_of = [&](int p) { return (brev(p >> lg2, lg1) << lg2) | brev(p & n2m, lg2); };
   const long long total = (long long)N * Kp;
+  if (N <= 64) {  // fragment order: e = ((cb Q + i) 64 + lane) 2 + s, Q = N / 8 16-byte loads per block and table
+    const int Q = N / 8, NT = N / 16;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (long long)gridDim.x * blockDim.x) {
+      const int s = (int)(e & 1), lane = (int)((e >> 1) & 63);
+      const long long g = e >> 7;
+      const int i = (int)(g % Q), cb = (int)(g / Q);
+      const int j = 2 * i + s;
+      {  // lp: t = j, bin 4t + lane/16, comp 16cb + lane%16
+        const int p = 4 * j + (lane >> 4), k = 16 * cb + (lane & 15);
+        const bool ok = k < K;
+        const long long src = (long long)bin_of(p) * K + k;
+        pr[e] = ok ? -rinvT[src] : 0.0;
+        if (has_mean) {
+          pur[e] = ok ? 2.0 * uT[src].x : 0.0;
+          pui[e] = ok ? 2.0 * uT[src].y : 0.0;
+        }
+      }
+      {  // filter: r = j / NT, t = j % NT; comp 16cb + lane/16 + 4r, bin 16t + lane%16
+        const int r = j / NT, t = j % NT;
+        const int k = 16 * cb + (lane >> 4) + 4 * r, p = 16 * t + (lane & 15);
+        const bool ok = k < K;
+        const long long src = (long long)k * N + bin_of(p);
+        pw[e] = ok ? wT[src] : 0.0;
+        if (has_mean) {
+          pbr[e] = ok ? bT[src].x : 0.0;
+          pbi[e] = ok ? bT[src].y : 0.0;
+        }
+      }
+      if (e < Kp) pc[e] = e < K ? cprime[e] : -__builtin_inf();
+    }
+    return;
+  }
   for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (long long)gridDim.x * blockDim.x) {
     {  // N x Kp
       const int p = (int)(e / Kp), k = (int)(e % Kp);
@@ -350,12 +588,31 @@ hipError_t launch_mfma_t(const QceFftEstArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int N, int OUT, bool HM>
+hipError_t launch_wave_t(const QceFftEstArgs& a, hipStream_t st) {
+  const size_t lds = 128 * 16 + (size_t)4 * 16 * (N + 1) * 16;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_fft_wave<N, OUT, HM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int lg1 = __builtin_ctz(a.n1), lg2 = __builtin_ctz(a.n2);
+  const long long ntiles = (a.B + 15) / 16;
+  const long long slots = 2LL * (a.cu > 0 ? a.cu : 256);  // two workgroups (8 waves) per CU, persistent
+  const long long wgs = (ntiles + 3) / 4 < slots ? (ntiles + 3) / 4 : slots;
+  hipLaunchKernelGGL((k_fft_wave<N, OUT, HM>), dim3((unsigned)wgs), dim3(256), lds, st, a.B, ntiles, lg1, lg2, a.Kp,
+                     a.y, a.pr, a.pur, a.pui, a.pc, a.pw, a.pbr, a.pbi, a.h, a.om, a.os, a.oa);
+  return hipGetLastError();
+}
+
 template <int OUT, bool HM>
 hipError_t launch_mfma_out(const QceFftEstArgs& a, hipStream_t st) {
   switch (a.N) {
-    case 16: return launch_mfma_t<16, OUT, HM>(a, st);
-    case 32: return launch_mfma_t<32, OUT, HM>(a, st);
-    case 64: return launch_mfma_t<64, OUT, HM>(a, st);
+    case 16: return launch_wave_t<16, OUT, HM>(a, st);
+    case 32: return launch_wave_t<32, OUT, HM>(a, st);
+    case 64: return launch_wave_t<64, OUT, HM>(a, st);
     case 128: return launch_mfma_t<128, OUT, HM>(a, st);
     case 256: return launch_mfma_t<256, OUT, HM>(a, st);
     default: return hipErrorInvalidValue;

@@ -176,6 +176,7 @@ struct QceFftEstArgs {
   // MFMA kernel tables (qce_fft_mfma.hip, storage order, components padded to Kp)
   int Kp;
   const double *pr, *pur, *pui, *pc, *pw, *pbr, *pbi;
+  int cu;  // compute units of the device (persistent grid of k_fft_wave)
 };
 bool qce_fft_pow2(int v);
 int qce_fft_tile(int N, int K);  // 0: no tile fits (K too large)

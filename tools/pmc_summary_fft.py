@@ -1,0 +1,61 @@
+"""Summarise tools/pmc_fft.sh passes (<dir>/<pass>/run_counter_collection.csv) for k_fft_mfma.
+
+Derived numbers (MI355X_MICROARCH.md): effective clock = GRBM_GUI_ACTIVE / 8 / dispatch time; MFMA busy =
+SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8); HBM-side bytes = 2 x FETCH_SIZE + WRITE_SIZE
+(gfx950 FETCH_SIZE counts half of a wide streaming read); SQ wave-time buckets in quad-cycles.
+"""
+import csv
+import os
+import sys
+
+base = sys.argv[1]
+pat = sys.argv[2] if len(sys.argv) > 2 else "k_fft_mfma"
+
+
+def load(name):
+    f = os.path.join(base, name, "run_counter_collection.csv")
+    out, dur = {}, []
+    if not os.path.exists(f):
+        return out, dur
+    for r in csv.DictReader(open(f)):
+        if pat not in r["Kernel_Name"]:
+            continue
+        out.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+        dur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+    return {k: sum(v) / len(v) for k, v in out.items()}, dur
+
+
+res = {}
+for p in ("sq", "fetch", "write", "lds", "tcc", "inst"):
+    v, d = load(p)
+    res[p] = (v, d)
+    for k, x in sorted(v.items()):
+        print(f"[{p:5s}] {k:28s} {x:.6g}")
+sq, dsq = res["sq"]
+if sq:
+    t = sum(dsq) / len(dsq)
+    clk = sq["GRBM_GUI_ACTIVE"] / 8 / t
+    busy = sq["SQ_VALU_MFMA_BUSY_CYCLES"] / (1024 * sq["GRBM_GUI_ACTIVE"] / 8)
+    print(f"dispatch {t * 1e3:.4f} ms, effective clock {clk / 1e9:.3f} GHz, MFMA busy {busy:.3f}")
+    print(f"wave time split: wait {sq['SQ_WAIT_ANY'] / sq['SQ_WAVE_CYCLES']:.3f}, issue-stall "
+          f"{sq['SQ_WAIT_INST_ANY'] / sq['SQ_WAVE_CYCLES']:.3f}, active {sq['SQ_ACTIVE_INST_ANY'] / sq['SQ_WAVE_CYCLES']:.3f}")
+    print(f"mean resident waves per SIMD {sq['SQ_WAVE_CYCLES'] * 4 / (1024 * sq['GRBM_GUI_ACTIVE'] / 8):.2f}")
+f, w = res["fetch"][0].get("FETCH_SIZE"), res["write"][0].get("WRITE_SIZE")
+if f and w:
+    _, dd = res["fetch"]
+    t = sum(dd) / len(dd)
+    hbm = (2 * f + w) * 1024
+    print(f"FETCH {f * 1024 / 1e6:.1f} MB (x2 = {2 * f * 1024 / 1e6:.1f}), WRITE {w * 1024 / 1e6:.1f} MB, "
+          f"traffic {hbm / 1e6:.1f} MB per launch, {hbm / t / 1e9:.0f} GB/s over the dispatch")
+tcc = res["tcc"][0]
+if tcc:
+    h, m = tcc["TCC_HIT_sum"], tcc["TCC_MISS_sum"]
+    print(f"L2 hit rate {h / (h + m):.3f}")
+lds = res["lds"][0]
+if lds:
+    print(f"LDS bank conflicts / LDS active {lds['SQ_LDS_BANK_CONFLICT'] / max(lds['SQ_LDS_IDX_ACTIVE'], 1):.4f}")
+ins = res["inst"][0]
+if ins and sq:
+    nw = sq["SQ_WAVES"]
+    print("per wave: " + ", ".join(f"{k[3:]} {ins[k] / nw:.0f}" for k in ("SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD",
+                                                                        "SQ_INSTS_SALU", "SQ_INSTS_MFMA") if k in ins))
