@@ -7,6 +7,7 @@
 #include <string.h>
 
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/qce.h"
@@ -116,6 +117,14 @@ struct qce_model {
   DevBuf<int> f_bad;
   DevBuf<double> f_pr, f_pur, f_pui, f_pc, f_pw, f_pbr, f_pbi;  // qce_fft_mfma.hip tables
   int fft_mfma = 0;                                            // the MFMA kernel serves 'all' / partial
+  // host-I/O pipeline of qce_estimate: two pinned slots per direction, copy-in / copy-out streams
+  struct {
+    double2* pin_y[2] = {nullptr, nullptr};
+    double2* pin_h[2] = {nullptr, nullptr};
+    size_t cap_y = 0, cap_h = 0;  // elements per slot
+    hipStream_t s_in = nullptr, s_out = nullptr;
+    hipEvent_t ev_in[2] = {nullptr, nullptr}, ev_c[2] = {nullptr, nullptr}, ev_out[2] = {nullptr, nullptr};
+  } hp;
   // arguments of the last prepare (replayed for the dense tables qce_get_tables returns)
   struct {
     int M = 0, quant_kind = 0, n_levels = 0;
@@ -615,6 +624,17 @@ int qce_model_destroy(qce_model* m) {
   for (auto* b : {&m->f_ceig, &m->f_rinvT, &m->f_cprime, &m->f_wT, &m->f_gain}) b->release();
   for (auto* b : {&m->f_col0, &m->f_mspec, &m->f_uT, &m->f_bT}) b->release();
   m->f_bad.release();
+  for (int i = 0; i < 2; ++i) {
+    if (m->hp.pin_y[i]) (void)hipHostFree(m->hp.pin_y[i]);
+    if (m->hp.pin_h[i]) (void)hipHostFree(m->hp.pin_h[i]);
+    for (hipEvent_t ev : {m->hp.ev_in[i], m->hp.ev_c[i], m->hp.ev_out[i]})
+      if (ev) (void)hipEventDestroy(ev);
+  }
+  for (hipStream_t hs : {m->hp.s_in, m->hp.s_out})
+    if (hs) {
+      (void)hipStreamSynchronize(hs);
+      (void)hipStreamDestroy(hs);
+    }
   if (m->stream) (void)hipStreamDestroy(m->stream);
   delete m;
   return QCE_OK;
@@ -901,6 +921,120 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
   return QCE_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// memcpy split over a few host threads (pageable numpy buffer <-> pinned slot)
+void par_memcpy(void* dst, const void* src, size_t bytes) {
+  const size_t piece = (size_t)4 << 20;
+  int nt = (int)((bytes + piece - 1) / piece);
+  const int hw = (int)std::thread::hardware_concurrency();
+  const int cap = hw >= 16 ? 8 : (hw >= 4 ? hw / 2 : 1);
+  if (nt > cap) nt = cap;
+  if (nt <= 1) {
+    memcpy(dst, src, bytes);
+    return;
+  }
+  const size_t per = (bytes + nt - 1) / nt;
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) {
+    const size_t o = per * t;
+    if (o >= bytes) break;
+    const size_t n = (o + per > bytes) ? bytes - o : per;
+    th.emplace_back([=] { memcpy((char*)dst + o, (const char*)src + o, n); });
+  }
+  memcpy(dst, src, per < bytes ? per : bytes);
+  for (auto& x : th) x.join();
+}
+
+// rows per host-pipeline chunk; 0 = one shot (QCE_HOST_PIPELINE=0, or too small a batch to split)
+long long host_chunk_rows(const qce_model* m, long long B) {
+  const char* e = getenv("QCE_HOST_PIPELINE");
+  if (e && e[0] == '0') return 0;
+  const long long width = m->M > m->N ? m->M : m->N;
+  long long cap = ((long long)32 << 20) / (16 * width);  // <= 32 MB per slot and direction
+  long long c = (B + 3) / 4;
+  if (c > cap) c = cap;
+  c = (c + 255) / 256 * 256;
+  if (c < 4096) c = 4096;
+  return (B >= 2 * c) ? c : 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Host numpy I/O split into chunks: host copies into a pinned slot, H2D on a copy stream, the estimate on
+// the compute stream, D2H on a second copy stream into another pinned slot, host copy out -- chunk i's
+// transfers overlap chunk i-1's and i+1's compute (results identical: every sample is independent).
+static int estimate_host_pipelined(qce_model* m, const double* y, long long B, long long C, int mode,
+                                   double mode_param, double* h_out, hipStream_t st) {
+  auto& hp = m->hp;
+  const size_t M = (size_t)m->M, N = (size_t)m->N;
+  if (!hp.s_in) HIPCHK(hipStreamCreateWithFlags(&hp.s_in, hipStreamNonBlocking));
+  if (!hp.s_out) HIPCHK(hipStreamCreateWithFlags(&hp.s_out, hipStreamNonBlocking));
+  for (int i = 0; i < 2; ++i) {
+    if (!hp.ev_in[i]) HIPCHK(hipEventCreateWithFlags(&hp.ev_in[i], hipEventDisableTiming));
+    if (!hp.ev_c[i]) HIPCHK(hipEventCreateWithFlags(&hp.ev_c[i], hipEventDisableTiming));
+    if (!hp.ev_out[i]) HIPCHK(hipEventCreateWithFlags(&hp.ev_out[i], hipEventDisableTiming));
+  }
+  if (hp.cap_y < (size_t)C * M || hp.cap_h < (size_t)C * N) {
+    HIPCHK(hipStreamSynchronize(hp.s_in));
+    HIPCHK(hipStreamSynchronize(hp.s_out));
+    for (int i = 0; i < 2; ++i) {
+      if (hp.pin_y[i]) (void)hipHostFree(hp.pin_y[i]);
+      if (hp.pin_h[i]) (void)hipHostFree(hp.pin_h[i]);
+      hp.pin_y[i] = hp.pin_h[i] = nullptr;
+    }
+    hp.cap_y = hp.cap_h = 0;
+    for (int i = 0; i < 2; ++i) {
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&hp.pin_y[i]), sizeof(double2) * (size_t)C * M, hipHostMallocDefault));
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&hp.pin_h[i]), sizeof(double2) * (size_t)C * N, hipHostMallocDefault));
+    }
+    hp.cap_y = (size_t)C * M;
+    hp.cap_h = (size_t)C * N;
+  }
+  HIPCHK(m->y_scr.ensure((size_t)B * M));
+  HIPCHK(m->h_scr.ensure((size_t)B * N));
+  const long long nc = (B + C - 1) / C;
+  const double2* ys = reinterpret_cast<const double2*>(y);
+  double2* hs = reinterpret_cast<double2*>(h_out);
+  int rc = QCE_OK;
+  for (long long i = 0; i <= nc; ++i) {
+    if (i < nc && rc == QCE_OK) {
+      const int s = (int)(i & 1);
+      const long long o = i * C, n = (B - o) < C ? (B - o) : C;
+      if (i >= 2) HIPCHK(hipEventSynchronize(hp.ev_in[s]));  // slot s: chunk i-2's upload has read it
+      par_memcpy(hp.pin_y[s], ys + o * M, sizeof(double2) * (size_t)n * M);
+      HIPCHK(hipMemcpyAsync(m->y_scr.p + o * M, hp.pin_y[s], sizeof(double2) * (size_t)n * M, hipMemcpyHostToDevice,
+                            hp.s_in));
+      HIPCHK(hipEventRecord(hp.ev_in[s], hp.s_in));
+      HIPCHK(hipStreamWaitEvent(st, hp.ev_in[s], 0));
+      rc = qce_estimate(m, reinterpret_cast<const double*>(m->y_scr.p + o * M), n, mode, mode_param,
+                        reinterpret_cast<double*>(m->h_scr.p + o * N), QCE_IO_DEVICE, st);
+      if (rc == QCE_OK) {
+        HIPCHK(hipEventRecord(hp.ev_c[s], st));
+        HIPCHK(hipStreamWaitEvent(hp.s_out, hp.ev_c[s], 0));
+        HIPCHK(hipMemcpyAsync(hp.pin_h[s], m->h_scr.p + o * N, sizeof(double2) * (size_t)n * N, hipMemcpyDeviceToHost,
+                              hp.s_out));
+        HIPCHK(hipEventRecord(hp.ev_out[s], hp.s_out));
+      }
+    }
+    if (i >= 1 && rc == QCE_OK) {  // chunk i-1 back to the caller's array
+      const long long j = i - 1, o = j * C, n = (B - o) < C ? (B - o) : C;
+      const int s = (int)(j & 1);
+      HIPCHK(hipEventSynchronize(hp.ev_out[s]));
+      par_memcpy(hs + o * N, hp.pin_h[s], sizeof(double2) * (size_t)n * N);
+    }
+  }
+  HIPCHK(hipStreamSynchronize(hp.s_in));
+  HIPCHK(hipStreamSynchronize(hp.s_out));
+  if (rc) return rc;
+  HOST_SYNC_CHECK(m, st);
+  return QCE_OK;
+}
+
 int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode_param, double* h_out, int io,
                  void* stream) {
   int rc = check_model(m, true);
@@ -912,6 +1046,9 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
   if (mode != QCE_MODE_ALL && m->K > 256) return fail(QCE_ENOTIMPL, "selective modes support K <= 256");
   DeviceGuard g(m->device);
   hipStream_t st = pick_stream(m, stream);
+  if (io == QCE_IO_HOST)
+    if (const long long C = host_chunk_rows(m, B))
+      return estimate_host_pipelined(m, y, B, C, mode, mode_param, h_out, st);
   const double2* dy = nullptr;
   if ((rc = stage_input(m, y, B, io, st, &dy))) return rc;
   double2* dh = reinterpret_cast<double2*>(h_out);

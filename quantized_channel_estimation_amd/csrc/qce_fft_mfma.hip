@@ -307,6 +307,36 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
   for (int e = tid; e < rows * N; e += 256) ht[e] = T[(e >> lgN) * RS + (e & (N - 1))];
 }
 
+// Reductions over the four 16-lane rows of a wave (lanes l, l^16, l^32, l^48) on the gfx950 cross-row
+// swaps (no LDS round trip): op(swap pair) = op(x[l], x[l^16]) in either operand order, so every row of a
+// column gets bit-identical results.
+QCE_DEV void row_pair(double v, bool r32, double& a, double& b) {
+  const int lo = __double2loint(v), hi = __double2hiint(v);
+  if (r32) {
+    const auto pl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto ph = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a = __hiloint2double(ph[0], pl[0]);
+    b = __hiloint2double(ph[1], pl[1]);
+  } else {
+    const auto pl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto ph = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    a = __hiloint2double(ph[0], pl[0]);
+    b = __hiloint2double(ph[1], pl[1]);
+  }
+}
+QCE_DEV double col_max4(double v) {
+  double a, b;
+  row_pair(v, false, a, b);
+  row_pair(fmax(a, b), true, a, b);
+  return fmax(a, b);
+}
+QCE_DEV double col_sum4(double v) {
+  double a, b;
+  row_pair(v, false, a, b);
+  row_pair(a + b, true, a, b);
+  return a + b;
+}
+
 // N <= 64: one wave owns 16 observations end to end (load, FFT, both products, IFFT, store) with no
 // workgroup barrier after the twiddle table; waves loop over 16-observation tiles (persistent grid of
 // two workgroups per CU, 8 waves per CU).  The spectra stay in the wave's LDS tile through the component
@@ -374,22 +404,12 @@ __global__ __launch_bounds__(256, 2) void k_fft_wave(long long B, long long ntil
         for (int r = 0; r < 4; ++r) Br[t][r] = Bi[t][r] = 0.0;
     }
     double m = -__builtin_inf(), ssum = 0.0;
-    double2 ta[NL], tb[NW];
-#pragma unroll
-    for (int i = 0; i < NL; ++i) ta[i] = PR[i * 64];
-#pragma unroll
-    for (int i = 0; i < NW; ++i) tb[i] = PW[i * 64];
-    for (int cb = 0; cb < ncb; ++cb) {
-      const int c0 = cb << 4;
-      const int nb = (cb + 1 < ncb ? cb + 1 : cb);  // next block's operands (the last block re-reads its own)
-      double2 na[NL], nw[NW];
-#pragma unroll
-      for (int i = 0; i < NL; ++i) na[i] = PR[(nb * NL + i) * 64];
-#pragma unroll
-      for (int i = 0; i < NW; ++i) nw[i] = PW[(nb * NW + i) * 64];
+    // Software pipeline over component blocks: iteration cb issues the lp MFMAs of block cb+1 (independent
+    // of block cb's softmax VALU, so the two overlap), then block cb's softmax and filter MFMAs.
+    auto lp_block = [&](int cb, const double2* ta, const double* pcv) {
       f64x4 C;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) C[r] = pc[c0 + hq + 4 * r];
+      for (int r = 0; r < 4; ++r) C[r] = pcv[r];
 #pragma unroll
       for (int i = 0; i < NL; ++i) {
         C = mfma16x16x4d(ta[i].x, y2[2 * i], C);
@@ -408,24 +428,23 @@ __global__ __launch_bounds__(256, 2) void k_fft_wave(long long B, long long ntil
           C = mfma16x16x4d(ub.y, v1.y, C);
         }
       }
-      // online softmax over this block of 16 components
-      double bm = fmax(fmax(C[0], C[1]), fmax(C[2], C[3]));
-      bm = fmax(bm, __shfl_xor(bm, 16));
-      bm = fmax(bm, __shfl_xor(bm, 32));
+      return C;
+    };
+    // online softmax over one block of 16 components (rows hq + 4 r, all four lane groups of a column);
+    // branch-free: an all -inf prefix gives alpha = e = 0 through the 0 shift
+    auto softmax = [&](const f64x4& C, double* e) {
+      const double bm = col_max4(fmax(fmax(C[0], C[1]), fmax(C[2], C[3])));
       const double mn = fmax(m, bm);
-      double e[4], alpha = 1.0;
-      if (mn == -__builtin_inf()) {
-        e[0] = e[1] = e[2] = e[3] = 0.0;
-      } else {
-        alpha = exp(m - mn);
+      const double sh = (mn == -__builtin_inf()) ? 0.0 : mn;
+      const double alpha = exp(m - sh);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) e[r] = exp(C[r] - mn);
-      }
-      double ls = (e[0] + e[1]) + (e[2] + e[3]);
-      ls += __shfl_xor(ls, 16);
-      ls += __shfl_xor(ls, 32);
+      for (int r = 0; r < 4; ++r) e[r] = exp(C[r] - sh);
+      const double ls = col_sum4((e[0] + e[1]) + (e[2] + e[3]));
       ssum = ssum * alpha + ls;
       m = mn;
+      return alpha;
+    };
+    auto filter_block = [&](int cb, const double2* tb, const double* e, double alpha) {
 #pragma unroll
       for (int t = 0; t < NT; ++t) F[t] *= alpha;
 #pragma unroll
@@ -450,10 +469,44 @@ __global__ __launch_bounds__(256, 2) void k_fft_wave(long long B, long long ntil
           Bi[t] = mfma16x16x4d((j & 1) ? ub.y : ub.x, e[r], Bi[t]);
         }
       }
+    };
+    const int last = ncb - 1;
+    double2 ta[NL], tb[NW];
+    double pcv[4];
 #pragma unroll
-      for (int i = 0; i < NL; ++i) ta[i] = na[i];
+    for (int i = 0; i < NL; ++i) ta[i] = PR[i * 64];
 #pragma unroll
-      for (int i = 0; i < NW; ++i) tb[i] = nw[i];
+    for (int r = 0; r < 4; ++r) pcv[r] = pc[hq + 4 * r];
+    f64x4 C = lp_block(0, ta, pcv);
+    {
+      const int b1 = last > 0 ? 1 : 0;
+#pragma unroll
+      for (int i = 0; i < NL; ++i) ta[i] = PR[(b1 * NL + i) * 64];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pcv[r] = pc[16 * b1 + hq + 4 * r];
+#pragma unroll
+      for (int i = 0; i < NW; ++i) tb[i] = PW[i * 64];
+    }
+    // operand registers are refilled right after the MFMAs that read them: lp operands of block cb+2
+    // behind the lp MFMAs of cb+1, filter operands of cb+1 behind the filter MFMAs of cb
+    for (int cb = 0; cb < last; ++cb) {
+      const int b1 = cb + 1, b2 = (cb + 2 < last ? cb + 2 : last);
+      const f64x4 Cn = lp_block(b1, ta, pcv);
+#pragma unroll
+      for (int i = 0; i < NL; ++i) ta[i] = PR[(b2 * NL + i) * 64];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pcv[r] = pc[16 * b2 + hq + 4 * r];
+      double e[4];
+      const double alpha = softmax(C, e);
+      filter_block(cb, tb, e, alpha);
+#pragma unroll
+      for (int i = 0; i < NW; ++i) tb[i] = PW[(b1 * NW + i) * 64];
+      C = Cn;
+    }
+    {
+      double e[4];
+      const double alpha = softmax(C, e);
+      filter_block(last, tb, e, alpha);
     }
     // Z = Y f + bb in place (each (observation, bin) of the tile belongs to exactly one lane)
     const double sc = (OUT == 0) ? 1.0 / ssum : 1.0;
@@ -593,8 +646,8 @@ hipError_t launch_wave_t(const QceFftEstArgs& a, hipStream_t st) {
   const size_t lds = 128 * 16 + (size_t)4 * 16 * (N + 1) * 16;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_fft_wave<N, OUT, HM>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)lds);
+    hipError_t e = hipFuncSetAttribute((const void*)k_fft_wave<N, OUT, HM>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
@@ -602,10 +655,11 @@ hipError_t launch_wave_t(const QceFftEstArgs& a, hipStream_t st) {
   const long long ntiles = (a.B + 15) / 16;
   const long long slots = 2LL * (a.cu > 0 ? a.cu : 256);  // two workgroups (8 waves) per CU, persistent
   const long long wgs = (ntiles + 3) / 4 < slots ? (ntiles + 3) / 4 : slots;
-  hipLaunchKernelGGL((k_fft_wave<N, OUT, HM>), dim3((unsigned)wgs), dim3(256), lds, st, a.B, ntiles, lg1, lg2, a.Kp,
-                     a.y, a.pr, a.pur, a.pui, a.pc, a.pw, a.pbr, a.pbi, a.h, a.om, a.os, a.oa);
+  hipLaunchKernelGGL((k_fft_wave<N, OUT, HM>), dim3((unsigned)wgs), dim3(256), lds, st, a.B, ntiles, lg1, lg2,
+                     a.Kp, a.y, a.pr, a.pur, a.pui, a.pc, a.pw, a.pbr, a.pbi, a.h, a.om, a.os, a.oa);
   return hipGetLastError();
 }
+
 
 template <int OUT, bool HM>
 hipError_t launch_mfma_out(const QceFftEstArgs& a, hipStream_t st) {
