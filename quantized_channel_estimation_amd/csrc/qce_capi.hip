@@ -1653,11 +1653,20 @@ static int assigned_impl(qce_model* m, const double* y, int64_t B, const int64_t
       dh = (double2*)p;
     }
     if (ls == 2) {
-      void *T, *P, *bz;
+      void *T, *P, *bz, *bad;
       HIPCHK(sc.get(&T, sizeof(double2) * (size_t)m->K * m->N * (m->N + m->M)));
       HIPCHK(sc.get(&P, sizeof(double2) * (size_t)m->K * m->N * m->M));
       HIPCHK(sc.get(&bz, sizeof(double2) * (size_t)m->K * m->N));
-      HIPCHK(qce_launch_ls_pinv(m->K, m->N, m->M, m->Aeff.p, (double2*)T, (double2*)P, (double2*)bz, st));
+      HIPCHK(sc.get(&bad, sizeof(int) * (size_t)m->K));
+      HIPCHK(qce_launch_ls_pinv(m->K, m->N, m->M, 0, m->Aeff.p, (double2*)T, (double2*)P, (double2*)bz, (int*)bad, st));
+      std::vector<int> hb(m->K);
+      HIPCHK(hipMemcpyAsync(hb.data(), bad, sizeof(int) * (size_t)m->K, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      for (int k = 0; k < m->K; ++k)
+        if (hb[k])
+          return fail(QCE_ECHOL, "LS: A_eff of component " + std::to_string(k) +
+                                     " is not of full column rank (Gram matrix pivot " + std::to_string(hb[k] - 1) +
+                                     " vanishes)");
       HIPCHK(qce_launch_est_assigned(B, m->N, m->M, m->K, dy, dc, (const double2*)P, (const double2*)bz, dh, st));
     } else if (ls) HIPCHK(qce_launch_ls(B, m->N, m->M, dy, dc, m->Aeff.p, dh, st));
     else HIPCHK(qce_launch_est_assigned(B, m->N, m->M, m->K, dy, dc, m->W.p, m->bvec.p, dh, st));
@@ -1814,7 +1823,7 @@ int qce_rate_mf(const double* h_est, const double* h, int64_t B, int N, const do
   const size_t nb = (size_t)B * N, nn = (size_t)N * N;
   {
     StreamScratch sc(st);
-    void *dhe = (void*)h_est, *dh = (void*)h, *dbuss, *dcq, *T, *cqi, *bz, *rate, *sum;
+    void *dhe = (void*)h_est, *dh = (void*)h, *dbuss, *dcq, *T, *cqi, *bz, *rate, *sum, *bad;
     HIPCHK(sc.get(&dbuss, sizeof(double) * N));
     HIPCHK(sc.get(&dcq, sizeof(double2) * nn));
     HIPCHK(sc.get(&T, sizeof(double2) * nn * 2));
@@ -1822,6 +1831,7 @@ int qce_rate_mf(const double* h_est, const double* h, int64_t B, int N, const do
     HIPCHK(sc.get(&bz, sizeof(double2) * N));
     HIPCHK(sc.get(&rate, sizeof(double) * (size_t)B));
     HIPCHK(sc.get(&sum, sizeof(double)));
+    HIPCHK(sc.get(&bad, sizeof(int)));
     HIPCHK(hipMemcpyAsync(dbuss, buss, sizeof(double) * N, hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(dcq, Cq, sizeof(double2) * nn, hipMemcpyHostToDevice, st));
     if (io == QCE_IO_HOST) {
@@ -1830,12 +1840,15 @@ int qce_rate_mf(const double* h_est, const double* h, int64_t B, int N, const do
       HIPCHK(hipMemcpyAsync(dhe, h_est, sizeof(double2) * nb, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(dh, h, sizeof(double2) * nb, hipMemcpyHostToDevice, st));
     }
-    HIPCHK(qce_launch_ls_pinv(1, N, N, (const double2*)dcq, (double2*)T, (double2*)cqi, (double2*)bz, st));
+    HIPCHK(qce_launch_ls_pinv(1, N, N, 1, (const double2*)dcq, (double2*)T, (double2*)cqi, (double2*)bz, (int*)bad, st));
     HIPCHK(qce_launch_rate_mf(B, N, (const double2*)dhe, (const double2*)dh, (const double*)dbuss, (const double2*)dcq,
                               (const double2*)cqi, (double*)rate, (double*)sum, st));
     double r = 0.0;
+    int hb = 0;
     HIPCHK(hipMemcpyAsync(&r, sum, sizeof(double), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&hb, bad, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if (hb) return fail(QCE_ECHOL, "rate_mf: Cq is not positive definite (pivot " + std::to_string(hb - 1) + ")");
     out[0] = r / (double)B;
   }
   return QCE_OK;
@@ -1851,6 +1864,30 @@ int qce_synchronize(qce_model* m) {
 }  // extern "C"
 
 #ifdef QCE_STAMPS
+hipError_t qce_fft_set_stamps(unsigned long long* dev);
+// diagnostic build only: stamp buffer of k_fft_wave (n 64-bit words on the device; n = 0 frees it) and
+// its readback (8 segment cycle sums per wave of the launches since the last call with n > 0)
+extern "C" int qce_debug_fft_stamps(unsigned long long* out, long long n) {
+  static unsigned long long* d = nullptr;
+  static long long cap = 0;
+  if (n <= 0) {
+    if (d) (void)hipFree(d);
+    d = nullptr;
+    cap = 0;
+    return qce_fft_set_stamps(nullptr) == hipSuccess ? 0 : QCE_EHIP;
+  }
+  if (!d) {
+    if (hipMalloc(&d, sizeof(unsigned long long) * n) != hipSuccess) return QCE_EHIP;
+    cap = n;
+    if (hipMemset(d, 0, sizeof(unsigned long long) * n) != hipSuccess) return QCE_EHIP;
+    if (qce_fft_set_stamps(d) != hipSuccess) return QCE_EHIP;
+    return 0;
+  }
+  if (n > cap) n = cap;
+  if (hipDeviceSynchronize() != hipSuccess) return QCE_EHIP;
+  if (hipMemcpy(out, d, sizeof(unsigned long long) * n, hipMemcpyDeviceToHost) != hipSuccess) return QCE_EHIP;
+  return (int)n;
+}
 // diagnostic build only: per-wave segment cycles (8 per wave) of the last k_est_all_f64 launch
 extern "C" int qce_debug_f64_stamps(unsigned long long* out, long long n) {
   if (!g_f64_stamps) return QCE_ESTATE;

@@ -307,6 +307,29 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
   for (int e = tid; e < rows * N; e += 256) ht[e] = T[(e >> lgN) * RS + (e & (N - 1))];
 }
 
+// Diagnostic build only (-DQCE_STAMPS): per-wave cycle sums of k_fft_wave's segments (s_memtime) into
+// g_fft_stamps (qce_debug_fft_stamps); the product kernel executes no stamp.
+#ifdef QCE_STAMPS
+__device__ unsigned long long* g_fft_stamps = nullptr;
+#define FW_STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime();
+#define FW_STAMP(i)                                             \
+  do {                                                          \
+    __builtin_amdgcn_sched_barrier(0);                          \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          \
+    st_acc[(i)] += t_ - st_prev;                                \
+    st_prev = t_;                                               \
+    __builtin_amdgcn_sched_barrier(0);                          \
+  } while (0)
+#define FW_STAMP_FLUSH                                                                                  \
+  if (g_fft_stamps && lane == 0)                                                                        \
+    for (int i_ = 0; i_ < 8; ++i_) g_fft_stamps[((long long)blockIdx.x * 4 + wid) * 8 + i_] = st_acc[i_];
+#else
+#define FW_STAMP_DECL
+#define FW_STAMP(i)
+#define FW_STAMP_FLUSH
+#endif
+
 // Reductions over the four 16-lane rows of a wave (lanes l, l^16, l^32, l^48) on the gfx950 cross-row
 // swaps (no LDS round trip): op(swap pair) = op(x[l], x[l^16]) in either operand order, so every row of a
 // column gets bit-identical results.
@@ -344,8 +367,9 @@ QCE_DEV double col_sum4(double v) {
 // consecutive MFMAs are one 16-byte load, and block cb+1's operands are fetched while block cb computes.
 //   lp  table: [cb][t/2][lane][t&1] = -rinv[bin 4t + lane/16][comp 16cb + lane%16]       t < N/4
 //   filter   : [cb][j/2][lane][j&1] = w[comp 16cb + lane/16 + 4r][bin 16t + lane%16]     j = r NT + t
-template <int N, int OUT, bool HM>
-__global__ __launch_bounds__(256, 2) void k_fft_wave(long long B, long long ntiles, int lg1, int lg2, int Kp,
+// CIRC: one axis (n1 = 1, circulant), FFT passes resolved at compile time
+template <int N, int OUT, bool HM, bool CIRC>
+__global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wave(long long B, long long ntiles, int lg1, int lg2, int Kp,
                                                      const double2* __restrict__ y, const double* __restrict__ pr,
                                                      const double* __restrict__ pur, const double* __restrict__ pui,
                                                      const double* __restrict__ pc, const double* __restrict__ pw,
@@ -374,26 +398,49 @@ __global__ __launch_bounds__(256, 2) void k_fft_wave(long long B, long long ntil
   const int ncb = Kp >> 4;
   const double2* PR = reinterpret_cast<const double2*>(pr) + lane;
   const double2* PW = reinterpret_cast<const double2*>(pw) + lane;
-  for (long long tile = (long long)blockIdx.x * 4 + wid; tile < ntiles; tile += (long long)gridDim.x * 4) {
+  FW_STAMP_DECL
+  // y of the wave's next tile is fetched into registers behind the component loop of the current one
+  // (N/4 16-byte loads in flight, latency hidden by the filter epilogue, inverse FFT and store); rows
+  // past the batch end read a clamped (valid) row and are stored as 0
+  const long long tstride = (long long)gridDim.x * 4;
+  double2 v[N / 4];
+  auto load_y = [&](long long t) {
+    const long long bb = t * 16;
+    const int rr = (int)((B - bb) < 16 ? (B - bb) : 16);
+    const double2* yt = y + bb * N;
+#pragma unroll
+    for (int i = 0; i < N / 4; ++i) {
+      const int e = lane + 64 * i, r = e >> lgN;
+      v[i] = yt[(r < rr ? r : rr - 1) * N + (e & (N - 1))];
+    }
+  };
+  constexpr bool PREF = !HM;  // the mean terms' accumulators leave no registers for the prefetch
+  long long tile = (long long)blockIdx.x * 4 + wid;
+  if (PREF && tile < ntiles) load_y(tile);
+  for (; tile < ntiles; tile += tstride) {
     const long long b0 = tile * 16;
     const int rows = (int)((B - b0) < 16 ? (B - b0) : 16);
-    {
-      const double2* yt = y + b0 * N;
+    if (!PREF) load_y(tile);
 #pragma unroll
-      for (int i = 0; i < N / 4; ++i) {
-        const int e = lane + 64 * i, r = e >> lgN;
-        T[r * RS + (e & (N - 1))] = (r < rows) ? yt[e] : make_double2(0.0, 0.0);
-      }
+    for (int i = 0; i < N / 4; ++i) {
+      const int e = lane + 64 * i, r = e >> lgN;
+      T[r * RS + (e & (N - 1))] = (r < rows) ? v[i] : make_double2(0.0, 0.0);
     }
     wave_lds_sync();
-    fft_axis_passes<false, true>(T, 4, RS, lgN, lg2, 1, tw);
-    if (lg1 > 0) fft_axis_passes<false, true>(T, 4, RS, lgN, lg1, 1 << lg2, tw);
-    double y2[NK];
-#pragma unroll
-    for (int t = 0; t < NK; ++t) {
-      const double2 v = Trow[4 * t + hq];
-      y2[t] = v.x * v.x + v.y * v.y;
+    FW_STAMP(0);
+    if constexpr (CIRC) {
+      fft_axis_passes<false, true>(T, 4, RS, lgN, lgN, 1, tw);  // compile-time passes and indices
+    } else {
+      fft_axis_passes<false, true>(T, 4, RS, lgN, lg2, 1, tw);
+      if (lg1 > 0) fft_axis_passes<false, true>(T, 4, RS, lgN, lg1, 1 << lg2, tw);
     }
+    FW_STAMP(1);
+    // |Y|^2 (the lp B operand) is re-derived from the spectra in LDS per block instead of held in 2 N / 4
+    // registers: those registers carry the next tile's y instead
+    auto y2 = [&](int t) {
+      const double2 q = Trow[4 * t + hq];
+      return q.x * q.x + q.y * q.y;
+    };
     f64x4 F[NT], Br[HM ? NT : 1], Bi[HM ? NT : 1];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
@@ -412,8 +459,8 @@ __global__ __launch_bounds__(256, 2) void k_fft_wave(long long B, long long ntil
       for (int r = 0; r < 4; ++r) C[r] = pcv[r];
 #pragma unroll
       for (int i = 0; i < NL; ++i) {
-        C = mfma16x16x4d(ta[i].x, y2[2 * i], C);
-        C = mfma16x16x4d(ta[i].y, y2[2 * i + 1], C);
+        C = mfma16x16x4d(ta[i].x, y2(2 * i), C);
+        C = mfma16x16x4d(ta[i].y, y2(2 * i + 1), C);
       }
       if constexpr (HM) {
         const double2* qa = reinterpret_cast<const double2*>(pur) + lane + cb * NL * 64;
@@ -487,6 +534,7 @@ __global__ __launch_bounds__(256, 2) void k_fft_wave(long long B, long long ntil
 #pragma unroll
       for (int i = 0; i < NW; ++i) tb[i] = PW[i * 64];
     }
+    FW_STAMP(2);
     // operand registers are refilled right after the MFMAs that read them: lp operands of block cb+2
     // behind the lp MFMAs of cb+1, filter operands of cb+1 behind the filter MFMAs of cb
     for (int cb = 0; cb < last; ++cb) {
@@ -502,6 +550,14 @@ __global__ __launch_bounds__(256, 2) void k_fft_wave(long long B, long long ntil
 #pragma unroll
       for (int i = 0; i < NW; ++i) tb[i] = PW[(b1 * NW + i) * 64];
       C = Cn;
+    }
+    FW_STAMP(3);
+    if (!PREF) {
+    } else if (tile + tstride < ntiles) {
+      load_y(tile + tstride);
+    } else {  // define v on every path, so the consumed values are dead through the component loop
+#pragma unroll
+      for (int i = 0; i < N / 4; ++i) v[i] = make_double2(0.0, 0.0);
     }
     {
       double e[4];
@@ -526,9 +582,15 @@ __global__ __launch_bounds__(256, 2) void k_fft_wave(long long B, long long ntil
       om[b0 + col] = m;
       os[b0 + col] = ssum;
     }
+    FW_STAMP(4);
     wave_lds_sync();
-    if (lg1 > 0) fft_axis_passes<true, true>(T, 4, RS, lgN, lg1, 1 << lg2, tw);
-    fft_axis_passes<true, true>(T, 4, RS, lgN, lg2, 1, tw);
+    if constexpr (CIRC) {
+      fft_axis_passes<true, true>(T, 4, RS, lgN, lgN, 1, tw);
+    } else {
+      if (lg1 > 0) fft_axis_passes<true, true>(T, 4, RS, lgN, lg1, 1 << lg2, tw);
+      fft_axis_passes<true, true>(T, 4, RS, lgN, lg2, 1, tw);
+    }
+    FW_STAMP(5);
     if (OUT == 3) {
       float2* at = reinterpret_cast<float2*>(oa) + b0 * N;
 #pragma unroll
@@ -541,14 +603,27 @@ __global__ __launch_bounds__(256, 2) void k_fft_wave(long long B, long long ntil
       }
     } else {
       double2* ht = h + b0 * N;
+      if (rows == 16) {  // whole tile: no per-element guard, all LDS reads issued before the stores
+        double2 v[N / 4];
 #pragma unroll
-      for (int i = 0; i < N / 4; ++i) {
-        const int e = lane + 64 * i, r = e >> lgN;
-        if (r < rows) ht[e] = T[r * RS + (e & (N - 1))];
+        for (int i = 0; i < N / 4; ++i) {
+          const int e = lane + 64 * i;
+          v[i] = T[(e >> lgN) * RS + (e & (N - 1))];
+        }
+#pragma unroll
+        for (int i = 0; i < N / 4; ++i) ht[lane + 64 * i] = v[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < N / 4; ++i) {
+          const int e = lane + 64 * i, r = e >> lgN;
+          if (r < rows) ht[e] = T[r * RS + (e & (N - 1))];
+        }
       }
     }
+    FW_STAMP(6);
     wave_lds_sync();
   }
+  FW_STAMP_FLUSH
 }
 
 // natural-order per-bin tables of k_fft_prep -> the kernel's storage order (bit-reversed per axis),
@@ -641,23 +716,30 @@ hipError_t launch_mfma_t(const QceFftEstArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <int N, int OUT, bool HM>
-hipError_t launch_wave_t(const QceFftEstArgs& a, hipStream_t st) {
+template <int N, int OUT, bool HM, bool CIRC>
+hipError_t launch_wave_c(const QceFftEstArgs& a, hipStream_t st) {
   const size_t lds = 128 * 16 + (size_t)4 * 16 * (N + 1) * 16;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_fft_wave<N, OUT, HM>,
+    hipError_t e = hipFuncSetAttribute((const void*)k_fft_wave<N, OUT, HM, CIRC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const int lg1 = __builtin_ctz(a.n1), lg2 = __builtin_ctz(a.n2);
   const long long ntiles = (a.B + 15) / 16;
-  const long long slots = 2LL * (a.cu > 0 ? a.cu : 256);  // two workgroups (8 waves) per CU, persistent
+  // persistent: two workgroups (8 waves) per CU; with means one (their accumulators need the registers of
+  // two waves)
+  const long long slots = (HM ? 1LL : 2LL) * (a.cu > 0 ? a.cu : 256);
   const long long wgs = (ntiles + 3) / 4 < slots ? (ntiles + 3) / 4 : slots;
-  hipLaunchKernelGGL((k_fft_wave<N, OUT, HM>), dim3((unsigned)wgs), dim3(256), lds, st, a.B, ntiles, lg1, lg2,
+  hipLaunchKernelGGL((k_fft_wave<N, OUT, HM, CIRC>), dim3((unsigned)wgs), dim3(256), lds, st, a.B, ntiles, lg1, lg2,
                      a.Kp, a.y, a.pr, a.pur, a.pui, a.pc, a.pw, a.pbr, a.pbi, a.h, a.om, a.os, a.oa);
   return hipGetLastError();
+}
+
+template <int N, int OUT, bool HM>
+hipError_t launch_wave_t(const QceFftEstArgs& a, hipStream_t st) {
+  return a.n1 == 1 ? launch_wave_c<N, OUT, HM, true>(a, st) : launch_wave_c<N, OUT, HM, false>(a, st);
 }
 
 
@@ -697,3 +779,10 @@ hipError_t qce_launch_fft_mfma(const QceFftEstArgs& a, int out, hipStream_t st) 
   if (out == 3) return a.has_mean ? launch_mfma_out<3, true>(a, st) : launch_mfma_out<3, false>(a, st);
   return hipErrorInvalidValue;
 }
+
+#ifdef QCE_STAMPS
+// diagnostic build only: point k_fft_wave's stamp buffer at dev (8 x 64-bit per wave; nullptr = off)
+hipError_t qce_fft_set_stamps(unsigned long long* dev) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_fft_stamps), &dev, sizeof(dev));
+}
+#endif

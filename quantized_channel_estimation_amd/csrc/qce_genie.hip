@@ -81,12 +81,17 @@ hipError_t qce_launch_ls(long long B, int N, int M, const double2* y, const long
 // once by Gauss-Jordan elimination of the Hermitian positive-definite Gram matrix (no pivoting needed) on the
 // augmented N x (N + M) tableau [G | A_eff^H] held in device scratch; h_b = P_c y_b then runs on
 // k_est_assigned with a zero offset.  One workgroup per component; the tableau is O(K N (N + M)) bytes.
+// direct = 1 eliminates [A | I] for a Hermitian positive-definite N x N A instead (A^-1 without forming A^H A,
+// so the condition number is not squared: the Cq^-1 of the matched-filter rate).  A pivot that is not finite
+// or whose real part falls to <= 1e-13 x the largest diagonal entry (rank-deficient / not positive definite)
+// is reported through bad[c] = its index + 1; the host turns that into QCE_ECHOL.
 namespace {
 
-__global__ __launch_bounds__(256) void k_ls_pinv(int N, int M, const double2* __restrict__ Aeff,
+__global__ __launch_bounds__(256) void k_ls_pinv(int N, int M, int direct, const double2* __restrict__ Aeff,
                                                  double2* __restrict__ T, double2* __restrict__ P,
-                                                 double2* __restrict__ bzero) {
+                                                 double2* __restrict__ bzero, int* __restrict__ bad) {
   __shared__ double2 f[256];
+  __shared__ double dmax;
   const int c = blockIdx.x, tid = threadIdx.x;
   const int L = N + M;
   const double2* A = Aeff + (long long)c * M * N;  // (M, N) row-major
@@ -94,7 +99,9 @@ __global__ __launch_bounds__(256) void k_ls_pinv(int N, int M, const double2* __
   for (int idx = tid; idx < N * L; idx += 256) {
     const int i = idx / L, j = idx % L;
     double2 v = make_double2(0.0, 0.0);
-    if (j < N) {
+    if (direct) {
+      v = (j < N) ? A[(long long)i * N + j] : make_double2(j - N == i ? 1.0 : 0.0, 0.0);
+    } else if (j < N) {
       for (int m = 0; m < M; ++m) v = cadd(v, cmul(cconj(A[(long long)m * N + i]), A[(long long)m * N + j]));
     } else {
       v = cconj(A[(long long)(j - N) * N + i]);
@@ -103,8 +110,16 @@ __global__ __launch_bounds__(256) void k_ls_pinv(int N, int M, const double2* __
   }
   for (int i = tid; i < N; i += 256) bzero[(long long)c * N + i] = make_double2(0.0, 0.0);
   __syncthreads();
+  if (tid == 0) {
+    double d = 0.0;
+    for (int i = 0; i < N; ++i) d = fmax(d, Tc[(long long)i * L + i].x);
+    dmax = d;
+    bad[c] = 0;
+  }
+  __syncthreads();
   for (int p = 0; p < N; ++p) {
     const double2 piv = Tc[(long long)p * L + p];
+    if (tid == 0 && bad[c] == 0 && !(piv.x > 1e-13 * dmax && isfinite(piv.x) && isfinite(piv.y))) bad[c] = p + 1;
     const double ip = 1.0 / (piv.x * piv.x + piv.y * piv.y);
     const double2 inv = make_double2(piv.x * ip, -piv.y * ip);
     for (int r = tid; r < N; r += 256) f[r] = cmul(Tc[(long long)r * L + p], inv);
@@ -127,16 +142,16 @@ __global__ __launch_bounds__(256) void k_ls_pinv(int N, int M, const double2* __
 
 }  // namespace
 
-hipError_t qce_launch_ls_pinv(int K, int N, int M, const double2* Aeff, double2* T, double2* P, double2* bzero,
-                              hipStream_t st) {
-  if (N > 256) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_ls_pinv, dim3((unsigned)K), dim3(256), 0, st, N, M, Aeff, T, P, bzero);
+hipError_t qce_launch_ls_pinv(int K, int N, int M, int direct, const double2* Aeff, double2* T, double2* P,
+                              double2* bzero, int* bad, hipStream_t st) {
+  if (N > 256 || (direct && M != N)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_ls_pinv, dim3((unsigned)K), dim3(256), 0, st, N, M, direct, Aeff, T, P, bzero, bad);
   return hipGetLastError();
 }
 
 // Per-sample matched-filter rate of the scripts' LS branch (Bussgang_GMM.py:186-198): with v = B h_est_b,
 // e = B (h_b - h_est_b), B = diag(buss) and g = v^H Cq^-1:
-// rate_b = Re log2(1 + |g v|^2 / (g Cq g^H + |g e|^2)).  One wave per sample; Cq^-1 from k_ls_pinv.
+// rate_b = Re log2(1 + |g v|^2 / (g Cq g^H + |g e|^2)).  One wave per sample; Cq^-1 from k_ls_pinv (direct).
 namespace {
 
 __global__ __launch_bounds__(256) void k_rate_mf(long long B, int N, const double2* __restrict__ he,

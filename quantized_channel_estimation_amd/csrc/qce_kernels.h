@@ -276,5 +276,7 @@ hipError_t qce_launch_ls(long long B, int N, int M, const double2* y, const long
 // Pseudo-inverses P_c = (A_eff^H A_eff)^{-1} A_eff^H of full-column-rank A_eff (qce_genie.hip; LS.py general A)
 hipError_t qce_launch_rate_mf(long long B, int N, const double2* he, const double2* h, const double* buss,
                               const double2* Cq, const double2* Cqi, double* rate, double* sum, hipStream_t st);
-hipError_t qce_launch_ls_pinv(int K, int N, int M, const double2* Aeff, double2* T, double2* P, double2* bzero,
-                              hipStream_t st);
+// Gauss-Jordan inverse per component: direct = 0 -> (A^H A)^-1 A^H (M >= N), 1 -> A^-1 (A Hermitian PD, M == N);
+// bad[c] = first failing pivot + 1 (0 = ok)
+hipError_t qce_launch_ls_pinv(int K, int N, int M, int direct, const double2* Aeff, double2* T, double2* P,
+                              double2* bzero, int* bad, hipStream_t st);

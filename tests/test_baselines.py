@@ -122,3 +122,27 @@ def test_ls_kind_routes_pilot_matrices():
     assert _ls_kind(rng.standard_normal((8, 4)) + 0j) == "general"
     with pytest.raises(NotImplementedError):
         _ls_kind(rng.standard_normal((3, 4)) + 0j)
+
+
+@pytest.mark.gpu
+def test_gpu_ls_general_ill_conditioned_and_rank_deficient(bl):
+    """Gram-matrix pivots (qce_genie.hip k_ls_pinv): an ill-conditioned pilot matrix (cond ~1e4, unquantised,
+    30 dB) still matches lstsq; a rank-deficient one (two equal columns), where lstsq returns the
+    minimum-norm solution, is refused with ValueError instead of returning inf / NaN."""
+    from quantized_channel_estimation_amd.baselines import LS
+    rng = np.random.default_rng(11)
+    C = bl["C"]
+    N = C.shape[0]
+    M = 2 * N
+    U, _ = np.linalg.qr(rng.standard_normal((M, N)) + 1j * rng.standard_normal((M, N)))
+    V, _ = np.linalg.qr(rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N)))
+    A = U @ np.diag(np.logspace(0, -4, N)) @ V.conj().T
+    y = rng.standard_normal((30, M)) + 1j * rng.standard_normal((30, M))
+    ls = LS(30.0, chunk=16)
+    hg = ls.estimate_global(y, C, A, np.inf)
+    exp = _ls_general_expected([y], [C], A, 30.0, np.inf)[0]
+    assert rel_fro(hg, exp) < 1e-6  # Gauss-Jordan on A^H A: error ~ cond(A)^2 eps
+    A2 = A.copy()
+    A2[:, 1] = A2[:, 0]
+    with pytest.raises(ValueError, match="full column rank"):
+        ls.estimate_global(y, C, A2, np.inf)

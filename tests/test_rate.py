@@ -102,3 +102,25 @@ def test_gpu_mf_rate_vs_oracle(n_bits):
     r = rate.matched_filter_rate(he, h, g, Cq)
     ro = O.rate_mf(he, h, g, Cq)
     assert np.isfinite(r) and abs(r - ro) <= 1e-9 * abs(ro)
+
+
+@pytest.mark.gpu
+def test_gpu_mf_rate_ill_conditioned_cq_and_not_pd():
+    """Cq^-1 of the matched-filter rate is eliminated from [Cq | I] directly (no Cq^H Cq, so cond(Cq) is
+    not squared): an ill-conditioned Cq (cond 1e6) matches the loop restatement; an indefinite Cq raises."""
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import rate
+    h, he, _ = _data(B=200)
+    N = h.shape[1]
+    rng = np.random.default_rng(3)
+    Q, _ = np.linalg.qr(rng.standard_normal((N, N)) + 1j * rng.standard_normal((N, N)))
+    Cq = Q @ np.diag(np.logspace(0, -6, N)) @ Q.conj().T
+    Cq = 0.5 * (Cq + Cq.conj().T)
+    g = np.full(N, np.sqrt(2 / np.pi))
+    r = rate.matched_filter_rate(he, h, g, Cq)
+    ro = O.rate_mf(he, h, g, Cq)
+    assert np.isfinite(r) and abs(r - ro) <= 1e-6 * abs(ro)
+    Cbad = Cq.copy()
+    Cbad[0, 0] = -1.0
+    with pytest.raises(ValueError, match="positive definite"):
+        rate.matched_filter_rate(he, h, g, Cbad)
