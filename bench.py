@@ -228,9 +228,13 @@ def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
         fft_flops = (4.0 * k_local * N + 10.0 * N * math.log2(N)) * B  # D3: zero-mean FFT-path flops
         return dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
-                    kernel="k_fft_mfma", structure=f"block-circulant ({n1},{n2})" if n1 > 1 else "circulant",
+                    kernel="k_fft_wave" if N <= 64 else "k_fft_mfma",
+                    structure=f"block-circulant ({n1},{n2})" if n1 > 1 else "circulant",
                     kernel_ms=round(kern_ms, 4), bytes_per_launch=bytes_per_launch,
-                    fp64_flops_per_launch=fft_flops, fp64_tflops=round(fft_flops / (kern_ms * 1e-3) / 1e12, 3))
+                    fp64_flops_per_launch=fft_flops, fp64_tflops=round(fft_flops / (kern_ms * 1e-3) / 1e12, 3),
+                    fp64_frac=round(fft_flops / (kern_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
+                    note="HBM roofline per SURVEY D3 (32 N B per estimate); the kernel's binding resource is FP64 "
+                         "issue (4 K N MFMA + FFT VALU flops per estimate), reported as fp64_frac")
     flops = 16.0 * k_local * N * N * B  # 16 K M N real flops per estimate
     achieved = flops / (kern_ms * 1e-3) / 1e12
     if dm.precision == "f64" and N <= 128:

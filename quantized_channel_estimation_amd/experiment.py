@@ -4,9 +4,13 @@
 scripts' MSE and the statistical rate bound (rate.py).  Returns the script's (mse_list, rate_list) tables
 (rows = SNRs after the transpose of :313-314); writing CSV files is left to the caller.
 
-The LS branch's per-sample matched-filter rate (:186-198, rate.matched_filter_rate) is its own column
-"LS_glob_mf" (the script appends it to the previous method's rate row, rate_list[-2]); its statistical bound
-(:200-211) is "LS_glob_stat".
+Like the script, every method sees its own observation draw per SNR (:133, :172, :216, :285): four
+independent on-device noise streams (seeds seed + 1 + 4 i + j for SNR i, method j).  The MSE and rate of
+a method use its own observation.
+
+Table layout: the LS branch's per-sample matched-filter rate (:186-198, rate.matched_filter_rate) is its own
+column "LS_glob_mf" -- the script appends it to the previous method's rate row (rate_list[-2]), which a CSV
+consumer reading by position must account for; its statistical bound (:200-211) is "LS_glob_stat".
 """
 import copy
 import warnings
@@ -38,13 +42,14 @@ def run(n_antennas=64, n_components=64, n_summands_or_proba="all", n_path=1, n_b
         gmm.fit(h_train, blocks=blocks, zero_mean=zero_mean)
     for i, snr in enumerate(snrs):
         thr, lab, _ = quantizer[snr]
-        r = observe.get_observation_nbit(h_val, snr, None, n_bits, thr, lab, seed=seed + 1 + i, device=device)
+        r = [observe.get_observation_nbit(h_val, snr, None, n_bits, thr, lab, seed=seed + 1 + 4 * i + j,
+                                          device=device) for j in range(4)]
         est = BLMMSE(snr, device=device)
-        res = {"blmmse_glob": est.estimate_global(r, cov, None, n_bits, quantizer_type, quantizer[snr]),
-               "LS_glob": LS(snr, device=device).estimate_global(r, cov, None, n_bits, quantizer_type,
+        res = {"blmmse_glob": est.estimate_global(r[0], cov, None, n_bits, quantizer_type, quantizer[snr]),
+               "LS_glob": LS(snr, device=device).estimate_global(r[1], cov, None, n_bits, quantizer_type,
                                                                  quantizer[snr]),
-               "blmmse_genie": est.estimate_genie(r, t_val, None, n_bits, quantizer_type, quantizer[snr]),
-               "blmmse_gmm": copy.deepcopy(gmm).estimate_from_y(r, snr, n_antennas, None, n_summands_or_proba,
+               "blmmse_genie": est.estimate_genie(r[2], t_val, None, n_bits, quantizer_type, quantizer[snr]),
+               "blmmse_gmm": copy.deepcopy(gmm).estimate_from_y(r[3], snr, n_antennas, None, n_summands_or_proba,
                                                                  n_bits, quantizer_type, quantizer[snr])}
         for k, v in res.items():
             mse[k].append(observe.mse(v, h_val, device=device))
