@@ -73,6 +73,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline budget per leg (0 = skip)")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the fast-path and drop-in side lines")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="CPU rehearsal of the launcher: ranks rendezvous over gloo, barrier + MAX-over-ranks "
+                         "timing, rank 0 prints one JSON line; no GPU is touched")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_metric.json"),
                     help="JSON with PMC-derived HBM bytes per launch of the estimate kernel")
     a = ap.parse_args()
@@ -113,6 +116,34 @@ def launch_ranks(n):
                     q.kill()
         time.sleep(0.05)
     return rc
+
+
+def launch_check(args):
+    """The multi-rank skeleton of main() without a GPU: rendezvous, barrier, per-rank timing reduced with
+    MAX, one JSON line from rank 0 (tests/test_sharding_cpu.py runs it at world size 2 over gloo)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    if world > 1:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    elapsed = 0.01 * (rank + 1)
+    t = torch.tensor([elapsed, float(rank)], dtype=torch.float64)
+    ranks = [rank]
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        out = [None] * world
+        dist.all_gather_object(out, rank)
+        ranks = out
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": args.gpus, "world_size": world, "ranks": ranks,
+                          "max_elapsed": float(t[0])}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
 
 
 # ------------------------------------------------------------------------------------------ inputs
@@ -317,6 +348,8 @@ def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
+    if args.launch_check:
+        return launch_check(args)
     cfg = dict(CONFIGS[args.config])
     if cfg.pop("dense", False):
         os.environ["QCE_FFT"] = "0"  # read by qce_prepare: keep the structured mixture on the dense path

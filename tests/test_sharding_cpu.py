@@ -205,3 +205,22 @@ def test_chunk_bounds_cover():
                     assert all(x[1] == y[0] for x, y in zip(b, b[1:]))
                     if sc:
                         assert all((hi - lo) % world == 0 for lo, hi in b[:-1])
+
+
+def test_bench_launcher_gloo_world2():
+    """`bench.py --gpus 2` starts its own two ranks (before any GPU call), they rendezvous on 127.0.0.1,
+    reduce the per-rank time with MAX and rank 0 prints one JSON line (CPU rehearsal, gloo)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--launch-check"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(line) == 1, r.stdout
+    d = json.loads(line[0])
+    assert d["world_size"] == 2 and d["n_gpus"] == 2 and sorted(d["ranks"]) == [0, 1]
+    assert abs(d["max_elapsed"] - 0.02) < 1e-12
