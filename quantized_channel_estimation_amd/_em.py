@@ -67,8 +67,12 @@ class DeviceEM:
         """estimate_gaussian_parameters (:698-737) on the device; resp None = the last E-step's."""
         torch = _torch()
         reg = self.reg if reg is None else float(reg)
-        R = self.R if resp is None else torch.as_tensor(np.ascontiguousarray(resp, dtype=np.float64),
-                                                        device=self.dev)
+        if resp is None:
+            R = self.R
+        elif isinstance(resp, torch.Tensor):  # device responsibilities of another DeviceEM on this GPU
+            R = resp.contiguous()
+        else:
+            R = torch.as_tensor(np.ascontiguousarray(resp, dtype=np.float64), device=self.dev)
         _lib.check(_lib.load().qce_em_mstep(_lib.ptr(self.X), self.B, self.N, self.K, _lib.ptr(R), reg,
                                             int(self.diag), int(self.zero_mean), _lib.ptr(self.nk),
                                             _lib.ptr(self.mu), _lib.ptr(self.cov), self.device, _lib.IO_DEVICE,

@@ -412,8 +412,23 @@ class Gmm_quant(Gmm_nbit):
         self.precisions_cholesky_quant = None
 
     def fit(self, h, n_bits, sigma2, quantizer, quant_type, blocks=None, zero_mean=False):
-        raise NotImplementedError("Gmm_quant.fit (EM with covariance recovery) is outside the MI355X estimate path; "
-                                  "fit with the reference and adopt the model with Gmm_quant.from_reference(fitted)")
+        """EM on quantised observations with covariance recovery (gmm_cplx_quant.py:103-189, 'full'
+        branch :155-159): device E-step on covariances_quant and device moments, the recovery algebra on the
+        host (_em_quant.py).  Other covariance types raise NotImplementedError."""
+        from . import _em_quant
+        self.params["zero_mean"] = bool(zero_mean)
+        self.n_bits, self.sigma2, self.quantizer, self.quant_type = n_bits, sigma2, quantizer, quant_type
+        if self.gm.covariance_type != "full":
+            raise NotImplementedError(f"Gmm_quant.fit on the device covers covariance_type 'full', not "
+                                      f"{self.gm.covariance_type!r}")
+        self._dev = None
+        self._dev_key = None
+        self._state = None
+        _em_quant.fit_predict(self, np.asarray(h))
+        self.means_cplx = self.gm.means_.copy()
+        self.covs_cplx = self.gm.covariances_.copy()
+        self.chol = self.gm.precisions_cholesky_.copy()
+        return self
 
     def _allow_inf(self):
         return False

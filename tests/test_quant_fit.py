@@ -1,0 +1,143 @@
+"""Gmm_quant.fit -- EM on quantised observations with covariance recovery ('full'; reference
+gmm_cplx_quant.py:103-189, :484-854, cov_est_quant.py:31-88) -- against tests/golden/quant_fit.npz, made
+by make_golden_quant_fit.py from the reference's own fits (1-bit, 2-bit uniform and 3-bit Lloyd-Max with
+zero means, unquantised and 1-bit with means).
+
+CPU: the control flow and the host-side recovery algebra of _em_quant.py driven by a NumPy backend (the
+oracle's E-step, M-step and gains) reproduce the reference's fits.  GPU: the same with the E-step, the
+weighted moments of the data and of its sign / threshold transforms, and the Bussgang gains on the
+device."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, rel_fro
+
+TAGS = ["b1_zm", "b2u_zm", "b3l_zm", "inf_mean", "b1_mean"]
+
+
+@pytest.fixture(scope="module")
+def qf():
+    return dict(np.load(os.path.join(GOLDEN, "quant_fit.npz"), allow_pickle=False))
+
+
+def _case(qf, tag):
+    p = tag + "__"
+    nb, zm, K, max_iter, snr, sigma2 = qf[p + "cfg"]
+    n_bits = np.inf if np.isinf(nb) else int(nb)
+    qt = str(qf[p + "qtype"])
+    quantizer = (qf[p + "thr"], qf[p + "lab"], None) if (p + "thr") in qf else (None, None, None)
+    return qf[p + "y"], n_bits, qt, quantizer, bool(zm), int(K), int(max_iter), float(sigma2)
+
+
+class NumpyBackend:
+    """The B-sized work of _em_quant on the CPU with the oracle's restatements (test infrastructure)."""
+
+    def __init__(self, X, K, zero_mean, n_bits, sigma2, quantizer, qt):
+        self.X, self.K, self.zm = X, K, zero_mean
+        self.n_bits, self.sigma2, self.quantizer, self.qt = n_bits, sigma2, quantizer, qt
+        self.R = None
+
+    def estep(self, means, covs, weights):
+        from oracle import qce_oracle as O
+        P = O.precision_cholesky(covs)
+        norm, log_resp = O.log_prob_resp(self.X, means, P, weights)
+        self.R = np.exp(log_resp)
+        return float(np.mean(norm))
+
+    def mstep(self, resp=None):
+        from oracle import qce_oracle as O
+        return O.em_mstep(self.X, self.R if resp is None else resp, 0.0, "full", self.zm)
+
+    def moments(self, resp=None):
+        from quantized_channel_estimation_amd._em_quant import _positive_thresholds
+        R = self.R if resp is None else resp
+        X = self.X
+        nk = R.sum(axis=0) + 10 * np.finfo(float).eps
+        S = (np.sign(X.real) + 1j * np.sign(X.imag)) / np.sqrt(2)
+        corr = np.stack([np.dot(R[:, k] * S.T, S.conj()) / nk[k] for k in range(self.K)])
+        thr = _positive_thresholds(self.quantizer[0])
+        probs = np.zeros((self.K, X.shape[1], thr.shape[0], 2))
+        for b, t in enumerate(thr):
+            probs[:, :, b, 0] = (R.T @ (np.abs(X.real) < t)) / nk[:, None]
+            probs[:, :, b, 1] = (R.T @ (np.abs(X.imag) < t)) / nk[:, None]
+        return corr, probs
+
+    def gains(self, covs):
+        from oracle import qce_oracle as O
+        snr = -10 * np.log10(self.sigma2)
+        out = []
+        for c in covs:
+            d = np.real(np.diag(c + self.sigma2 * np.eye(c.shape[0])))
+            g = O.gain_lloyd(self.n_bits, d, self.quantizer[0], self.quantizer[1]) if self.qt == "lloyd" else \
+                O.gain_uniform(snr, self.n_bits, d)
+            out.append(np.asarray(g, dtype=complex))
+        return np.stack(out)
+
+    def labels(self):
+        return self.R.argmax(axis=1)
+
+    def precision_cholesky(self, covs):
+        from oracle import qce_oracle as O
+        return O.precision_cholesky(covs)
+
+
+def _check(qf, tag, g, tol):
+    p = tag + "__"
+    assert int(g.gm.n_iter_) == int(qf[p + "n_iter"])
+    assert bool(g.gm.converged_) == bool(qf[p + "converged"])
+    assert abs(g.gm.lower_bound_ - float(qf[p + "lower_bound"])) <= tol * abs(float(qf[p + "lower_bound"]))
+    assert rel_fro(g.gm.weights_, qf[p + "weights"]) < tol
+    if np.abs(qf[p + "means"]).max() > 0:
+        assert rel_fro(g.means_cplx, qf[p + "means"]) < tol
+    else:
+        assert np.abs(g.means_cplx).max() == 0
+    assert rel_fro(g.covs_cplx, qf[p + "covs"]) < tol
+    assert rel_fro(g.covariances_quant, qf[p + "covs_quant"]) < tol
+    assert rel_fro(g.chol, qf[p + "chol"]) < tol
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_quant_fit_numpy_backend_matches_reference(qf, tag, capsys):
+    import warnings
+    from threadpoolctl import threadpool_limits
+    from quantized_channel_estimation_amd import Gmm_quant, _em_quant
+    y, n_bits, qt, quantizer, zm, K, max_iter, sigma2 = _case(qf, tag)
+    g = Gmm_quant(n_components=K, covariance_type="full", max_iter=max_iter, random_state=0)
+    g.params["zero_mean"] = zm
+    g.n_bits, g.sigma2, g.quantizer, g.quant_type = n_bits, sigma2, quantizer, qt
+    be = NumpyBackend(np.asarray(y, complex), K, zm, n_bits, sigma2, quantizer, qt)
+    np.random.seed(123)
+    with threadpool_limits(limits=1), warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        _em_quant.fit_predict(g, y, backend=be)
+    g.means_cplx, g.covs_cplx, g.chol = g.gm.means_, g.gm.covariances_, g.gm.precisions_cholesky_
+    _check(qf, tag, g, 1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", TAGS)
+def test_gpu_quant_fit_matches_reference(qf, tag):
+    import warnings
+    from threadpoolctl import threadpool_limits
+    from quantized_channel_estimation_amd import Gmm_quant, _lib
+    if _lib.device_count() == 0:
+        pytest.fail("no GPU visible for a gpu-marked test")
+    y, n_bits, qt, quantizer, zm, K, max_iter, sigma2 = _case(qf, tag)
+    g = Gmm_quant(n_components=K, covariance_type="full", max_iter=max_iter, random_state=0)
+    np.random.seed(123)
+    with threadpool_limits(limits=1), warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        g.fit(h=y, n_bits=n_bits, sigma2=sigma2, quantizer=quantizer, quant_type=qt, zero_mean=zm)
+    _check(qf, tag, g, 1e-7)
+    # the fitted model estimates through the product kernels
+    hq = g.estimate_from_y(y[:32], -10 * np.log10(sigma2), y.shape[1], None, "all", n_bits, qt, quantizer)
+    assert np.isfinite(hq).all()
+
+
+def test_quant_fit_refuses_other_covariance_types():
+    from quantized_channel_estimation_amd import Gmm_quant
+    g = Gmm_quant(n_components=2, covariance_type="circulant")
+    with pytest.raises(NotImplementedError):
+        g.fit(h=np.ones((10, 4), complex), n_bits=1, sigma2=0.1, quantizer=(None, None, None), quant_type="uniform")
