@@ -162,12 +162,21 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
     sincospi(-(double)t / 128.0, &sn, &cs);
     tw[t] = make_double2(cs, sn);
   }
-  {
+  {  // all TS N / 256 loads per thread in flight at once: rows past the batch end read a clamped (valid)
+     // row and are stored as 0
+    static_assert(TS * N % 256 == 0, "tile");
+    constexpr int NL = TS * N / 256;
     const double2* yt = y + b0 * N;
-#pragma unroll 4
-    for (int e = tid; e < TS * N; e += 256) {
-      const int r = e >> lgN;
-      T[r * RS + (e & (N - 1))] = (r < rows) ? yt[e] : make_double2(0.0, 0.0);
+    double2 v[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int e = tid + 256 * i, r = e >> lgN;
+      v[i] = yt[(r < rows ? r : rows - 1) * N + (e & (N - 1))];
+    }
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int e = tid + 256 * i, r = e >> lgN;
+      T[r * RS + (e & (N - 1))] = (r < rows) ? v[i] : make_double2(0.0, 0.0);
     }
   }
   __syncthreads();
@@ -191,8 +200,26 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
     for (int r = 0; r < 4; ++r) Br[t][r] = Bi[t][r] = 0.0;
   double m = -__builtin_inf(), ssum = 0.0;
   const int ncb = Kp >> 4;
+  // zero-mean models: the table operands of block cb+1 are fetched while block cb computes (registers to
+  // spare); the mean variants load them in place
+  constexpr bool PF = !has_mean;
+  constexpr int NA = PF ? NB / 4 : 1, NWF = PF ? 4 * NT : 1;
+  double ca[NA], cw[NWF];
+  auto fetch = [&](int cb, double* a, double* w) {
+    const int c0 = cb << 4;
+    const double* pa = pr + (long long)(bin0 + hq) * Kp + c0 + col;
+#pragma unroll
+    for (int t = 0; t < NA; ++t) a[t] = pa[(long long)4 * t * Kp];
+#pragma unroll
+    for (int r = 0; r < 4 && PF; ++r)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) w[r * NT + t] = pw[(long long)(c0 + hq + 4 * r) * N + bin0 + col + 16 * t];
+  };
+  if constexpr (PF) fetch(0, ca, cw);
   for (int cb = 0; cb < ncb; ++cb) {
     const int c0 = cb << 4;
+    double na[NA], nw[NWF];
+    if constexpr (PF) fetch(cb + 1 < ncb ? cb + 1 : cb, na, nw);
     f64x4 C;
 #pragma unroll
     for (int r = 0; r < 4; ++r) C[r] = (kw == 0) ? pc[c0 + hq + 4 * r] : 0.0;
@@ -202,7 +229,7 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
 #pragma unroll
       for (int t = 0; t < NB / 4; ++t) {
         const double2 v = Trow[bin0 + 4 * t + hq];
-        C = mfma16x16x4d(pa[(long long)4 * t * Kp], v.x * v.x + v.y * v.y, C);
+        C = mfma16x16x4d(PF ? ca[PF ? t : 0] : pa[(long long)4 * t * Kp], v.x * v.x + v.y * v.y, C);
       }
       if constexpr (has_mean) {
         const double *qa = pur + o, *qb = pui + o;
@@ -260,7 +287,7 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
       const long long o = (long long)(c0 + hq + 4 * r) * N + bin0 + col;
       const double* wa = pw + o;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) F[t] = mfma16x16x4d(wa[16 * t], e[r], F[t]);
+      for (int t = 0; t < NT; ++t) F[t] = mfma16x16x4d(PF ? cw[PF ? r * NT + t : 0] : wa[16 * t], e[r], F[t]);
       if constexpr (has_mean) {
         const double *ba = pbr + o, *bb = pbi + o;
 #pragma unroll
@@ -269,6 +296,12 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
           Bi[t] = mfma16x16x4d(bb[16 * t], e[r], Bi[t]);
         }
       }
+    }
+    if constexpr (PF) {
+#pragma unroll
+      for (int t = 0; t < NA; ++t) ca[t] = na[t];
+#pragma unroll
+      for (int t = 0; t < NWF; ++t) cw[t] = nw[t];
     }
   }
   // Z = Y f + bb in place (each (observation, bin) of the tile belongs to exactly one lane)
@@ -303,6 +336,18 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
     return;
   }
   double2* ht = h + b0 * N;
+  if (rows == TS) {  // whole tile: all LDS reads issued before the unguarded stores
+    constexpr int NL = TS * N / 256;
+    double2 v[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int e = tid + 256 * i;
+      v[i] = T[(e >> lgN) * RS + (e & (N - 1))];
+    }
+#pragma unroll
+    for (int i = 0; i < NL; ++i) ht[tid + 256 * i] = v[i];
+    return;
+  }
 #pragma unroll 4
   for (int e = tid; e < rows * N; e += 256) ht[e] = T[(e >> lgN) * RS + (e & (N - 1))];
 }
