@@ -444,12 +444,16 @@ __global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wave(long long B, long 
   const double2* PR = reinterpret_cast<const double2*>(pr) + lane;
   const double2* PW = reinterpret_cast<const double2*>(pw) + lane;
   FW_STAMP_DECL
+  // Main phase: whole rounds of tiles, one wave per tile.  The remainder (fewer tiles than waves: the last,
+  // partial round at large B, every tile at small B) is worked by the four waves of a workgroup together,
+  // each on every fourth component block, with the partial (m, s, F) merged through LDS (zero-mean models)
+  const long long W = (long long)gridDim.x * 4;
+  const long long nmain = HM ? ntiles : (ntiles / W) * W;
   // y of the wave's next tile is fetched into registers behind the component loop of the current one
   // (N/4 16-byte loads in flight, latency hidden by the filter epilogue, inverse FFT and store); rows
   // past the batch end read a clamped (valid) row and are stored as 0
-  const long long tstride = (long long)gridDim.x * 4;
   double2 v[N / 4];
-  auto load_y = [&](long long t) {
+  auto load_y = [&](long long t) __attribute__((always_inline)) {
     const long long bb = t * 16;
     const int rr = (int)((B - bb) < 16 ? (B - bb) : 16);
     const double2* yt = y + bb * N;
@@ -460,12 +464,12 @@ __global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wave(long long B, long 
     }
   };
   constexpr bool PREF = !HM;  // the mean terms' accumulators leave no registers for the prefetch
-  long long tile = (long long)blockIdx.x * 4 + wid;
-  if (PREF && tile < ntiles) load_y(tile);
-  for (; tile < ntiles; tile += tstride) {
+  // one tile: component blocks s0, s0 + bs, ...; next >= 0: prefetch that tile's y (main phase);
+  // coop: the workgroup's four waves share the tile (bs = 4), wave 0 merges and writes
+  auto run_tile = [&](long long tile, int s0, int bs, long long next, bool coop) __attribute__((always_inline)) {
     const long long b0 = tile * 16;
     const int rows = (int)((B - b0) < 16 ? (B - b0) : 16);
-    if (!PREF) load_y(tile);
+    if (!PREF || coop) load_y(tile);
 #pragma unroll
     for (int i = 0; i < N / 4; ++i) {
       const int e = lane + 64 * i, r = e >> lgN;
@@ -496,8 +500,8 @@ __global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wave(long long B, long 
         for (int r = 0; r < 4; ++r) Br[t][r] = Bi[t][r] = 0.0;
     }
     double m = -__builtin_inf(), ssum = 0.0;
-    // Software pipeline over component blocks: iteration cb issues the lp MFMAs of block cb+1 (independent
-    // of block cb's softmax VALU, so the two overlap), then block cb's softmax and filter MFMAs.
+    // Software pipeline over component blocks: iteration j issues the lp MFMAs of block j+1 (independent
+    // of block j's softmax VALU, so the two overlap), then block j's softmax and filter MFMAs.
     auto lp_block = [&](int cb, const double2* ta, const double* pcv) {
       f64x4 C;
 #pragma unroll
@@ -562,112 +566,155 @@ __global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wave(long long B, long 
         }
       }
     };
-    const int last = ncb - 1;
-    double2 ta[NL], tb[NW];
-    double pcv[4];
+    const int nb = (ncb - s0 + bs - 1) / bs;  // this wave's component blocks s0 + j bs, j < nb
+    auto blk = [&](int j) { return s0 + j * bs; };
+    if (nb > 0) {
+      const int last = nb - 1;
+      double2 ta[NL], tb[NW];
+      double pcv[4];
 #pragma unroll
-    for (int i = 0; i < NL; ++i) ta[i] = PR[i * 64];
+      for (int i = 0; i < NL; ++i) ta[i] = PR[(blk(0) * NL + i) * 64];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) pcv[r] = pc[hq + 4 * r];
-    f64x4 C = lp_block(0, ta, pcv);
-    {
-      const int b1 = last > 0 ? 1 : 0;
+      for (int r = 0; r < 4; ++r) pcv[r] = pc[16 * blk(0) + hq + 4 * r];
+      f64x4 C = lp_block(blk(0), ta, pcv);
+      {
+        const int b1 = blk(last > 0 ? 1 : 0);
 #pragma unroll
-      for (int i = 0; i < NL; ++i) ta[i] = PR[(b1 * NL + i) * 64];
+        for (int i = 0; i < NL; ++i) ta[i] = PR[(b1 * NL + i) * 64];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) pcv[r] = pc[16 * b1 + hq + 4 * r];
+        for (int r = 0; r < 4; ++r) pcv[r] = pc[16 * b1 + hq + 4 * r];
 #pragma unroll
-      for (int i = 0; i < NW; ++i) tb[i] = PW[i * 64];
-    }
-    FW_STAMP(2);
-    // operand registers are refilled right after the MFMAs that read them: lp operands of block cb+2
-    // behind the lp MFMAs of cb+1, filter operands of cb+1 behind the filter MFMAs of cb
-    for (int cb = 0; cb < last; ++cb) {
-      const int b1 = cb + 1, b2 = (cb + 2 < last ? cb + 2 : last);
-      const f64x4 Cn = lp_block(b1, ta, pcv);
-#pragma unroll
-      for (int i = 0; i < NL; ++i) ta[i] = PR[(b2 * NL + i) * 64];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) pcv[r] = pc[16 * b2 + hq + 4 * r];
-      double e[4];
-      const double alpha = softmax(C, e);
-      filter_block(cb, tb, e, alpha);
-#pragma unroll
-      for (int i = 0; i < NW; ++i) tb[i] = PW[(b1 * NW + i) * 64];
-      C = Cn;
-    }
-    FW_STAMP(3);
-    if (!PREF) {
-    } else if (tile + tstride < ntiles) {
-      load_y(tile + tstride);
-    } else {  // define v on every path, so the consumed values are dead through the component loop
-#pragma unroll
-      for (int i = 0; i < N / 4; ++i) v[i] = make_double2(0.0, 0.0);
-    }
-    {
-      double e[4];
-      const double alpha = softmax(C, e);
-      filter_block(last, tb, e, alpha);
-    }
-    // Z = Y f + bb in place (each (observation, bin) of the tile belongs to exactly one lane)
-    const double sc = (OUT == 0) ? 1.0 / ssum : 1.0;
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int bin = 16 * t + hq + 4 * r;
-        const double2 v = Trow[bin];
-        const double f = F[t][r] * sc;
-        if constexpr (HM)
-          Trow[bin] = make_double2(fma(v.x, f, Br[t][r] * sc), fma(v.y, f, Bi[t][r] * sc));
-        else
-          Trow[bin] = make_double2(v.x * f, v.y * f);
+        for (int i = 0; i < NW; ++i) tb[i] = PW[(blk(0) * NW + i) * 64];
       }
-    if (OUT == 3 && hq == 0 && col < rows) {
-      om[b0 + col] = m;
-      os[b0 + col] = ssum;
-    }
-    FW_STAMP(4);
-    wave_lds_sync();
-    if constexpr (CIRC) {
-      fft_axis_passes<true, true>(T, 4, RS, lgN, lgN, 1, tw);
-    } else {
-      if (lg1 > 0) fft_axis_passes<true, true>(T, 4, RS, lgN, lg1, 1 << lg2, tw);
-      fft_axis_passes<true, true>(T, 4, RS, lgN, lg2, 1, tw);
-    }
-    FW_STAMP(5);
-    if (OUT == 3) {
-      float2* at = reinterpret_cast<float2*>(oa) + b0 * N;
+      FW_STAMP(2);
+      // operand registers are refilled right after the MFMAs that read them: lp operands of block j+2
+      // behind the lp MFMAs of j+1, filter operands of j+1 behind the filter MFMAs of j
+      for (int j = 0; j < last; ++j) {
+        const int b1 = blk(j + 1), b2 = blk(j + 2 < last ? j + 2 : last);
+        const f64x4 Cn = lp_block(b1, ta, pcv);
 #pragma unroll
-      for (int i = 0; i < N / 4; ++i) {
-        const int e = lane + 64 * i, r = e >> lgN;
-        if (r < rows) {
-          const double2 v = T[r * RS + (e & (N - 1))];
-          at[e] = make_float2((float)v.x, (float)v.y);
-        }
+        for (int i = 0; i < NL; ++i) ta[i] = PR[(b2 * NL + i) * 64];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pcv[r] = pc[16 * b2 + hq + 4 * r];
+        double e[4];
+        const double alpha = softmax(C, e);
+        filter_block(blk(j), tb, e, alpha);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) tb[i] = PW[(b1 * NW + i) * 64];
+        C = Cn;
       }
-    } else {
-      double2* ht = h + b0 * N;
-      if (rows == 16) {  // whole tile: no per-element guard, all LDS reads issued before the stores
-        double2 v[N / 4];
+      FW_STAMP(3);
+      if (PREF && next >= 0) {
+        load_y(next);
+      } else {  // define v on every path, so the consumed values are dead through the component loop
 #pragma unroll
-        for (int i = 0; i < N / 4; ++i) {
-          const int e = lane + 64 * i;
-          v[i] = T[(e >> lgN) * RS + (e & (N - 1))];
+        for (int i = 0; i < N / 4; ++i) v[i] = make_double2(0.0, 0.0);
+      }
+      {
+        double e[4];
+        const double alpha = softmax(C, e);
+        filter_block(blk(last), tb, e, alpha);
+      }
+    }
+    if (coop) {  // waves 1-3 hand (F, m, s) to wave 0 through their own (now free) spectra tiles
+      double* Td = reinterpret_cast<double*>(T);
+      if (wid != 0) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Td[(t * 4 + r) * 64 + lane] = F[t][r];
+        Td[4 * NT * 64 + lane] = m;
+        Td[(4 * NT + 1) * 64 + lane] = ssum;
+      }
+      __syncthreads();
+      if (wid == 0) {  // fixed order: wave 0's own partial, then waves 1, 2, 3
+        double mm = m;
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+          const double* Tw = reinterpret_cast<const double*>(tw + 128 + w * (16 * RS));
+          mm = fmax(mm, Tw[4 * NT * 64 + lane]);
         }
+        const double f0 = exp(m - mm);
+        ssum *= f0;
 #pragma unroll
-        for (int i = 0; i < N / 4; ++i) ht[lane + 64 * i] = v[i];
+        for (int t = 0; t < NT; ++t) F[t] *= f0;
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+          const double* Tw = reinterpret_cast<const double*>(tw + 128 + w * (16 * RS));
+          const double mw = Tw[4 * NT * 64 + lane];
+          const double fw = (mw == -__builtin_inf()) ? 0.0 : exp(mw - mm);
+          ssum = fma(Tw[(4 * NT + 1) * 64 + lane], fw, ssum);
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) F[t][r] = fma(Tw[(t * 4 + r) * 64 + lane], fw, F[t][r]);
+        }
+        m = mm;
+      }
+    }
+    if (!coop || wid == 0) {
+      // Z = Y f + bb in place (each (observation, bin) of the tile belongs to exactly one lane)
+      const double sc = (OUT == 0) ? 1.0 / ssum : 1.0;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int bin = 16 * t + hq + 4 * r;
+          const double2 q = Trow[bin];
+          const double f = F[t][r] * sc;
+          if constexpr (HM)
+            Trow[bin] = make_double2(fma(q.x, f, Br[t][r] * sc), fma(q.y, f, Bi[t][r] * sc));
+          else
+            Trow[bin] = make_double2(q.x * f, q.y * f);
+        }
+      if (OUT == 3 && hq == 0 && col < rows) {
+        om[b0 + col] = m;
+        os[b0 + col] = ssum;
+      }
+      FW_STAMP(4);
+      wave_lds_sync();
+      if constexpr (CIRC) {
+        fft_axis_passes<true, true>(T, 4, RS, lgN, lgN, 1, tw);
       } else {
+        if (lg1 > 0) fft_axis_passes<true, true>(T, 4, RS, lgN, lg1, 1 << lg2, tw);
+        fft_axis_passes<true, true>(T, 4, RS, lgN, lg2, 1, tw);
+      }
+      FW_STAMP(5);
+      if (OUT == 3) {
+        float2* at = reinterpret_cast<float2*>(oa) + b0 * N;
 #pragma unroll
         for (int i = 0; i < N / 4; ++i) {
           const int e = lane + 64 * i, r = e >> lgN;
-          if (r < rows) ht[e] = T[r * RS + (e & (N - 1))];
+          if (r < rows) {
+            const double2 q = T[r * RS + (e & (N - 1))];
+            at[e] = make_float2((float)q.x, (float)q.y);
+          }
+        }
+      } else {
+        double2* ht = h + b0 * N;
+        if (rows == 16) {  // whole tile: no per-element guard, all LDS reads issued before the stores
+#pragma unroll
+          for (int i = 0; i < N / 4; ++i) {
+            const int e = lane + 64 * i;
+            ht[e] = T[(e >> lgN) * RS + (e & (N - 1))];
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < N / 4; ++i) {
+            const int e = lane + 64 * i, r = e >> lgN;
+            if (r < rows) ht[e] = T[r * RS + (e & (N - 1))];
+          }
         }
       }
     }
+    if (coop) __syncthreads();  // wave 0 has read the partials before the next tile overwrites them
     FW_STAMP(6);
     wave_lds_sync();
-  }
+  };
+  long long tile = (long long)blockIdx.x * 4 + wid;
+  if (PREF && tile < nmain) load_y(tile);
+  for (; tile < nmain; tile += W) run_tile(tile, 0, 1, tile + W < nmain ? tile + W : -1, false);
+  for (long long tt = nmain + blockIdx.x; tt < ntiles; tt += gridDim.x) run_tile(tt, wid, 4, -1, true);
   FW_STAMP_FLUSH
 }
 
@@ -776,7 +823,10 @@ hipError_t launch_wave_c(const QceFftEstArgs& a, hipStream_t st) {
   // persistent: two workgroups (8 waves) per CU; with means one (their accumulators need the registers of
   // two waves)
   const long long slots = (HM ? 1LL : 2LL) * (a.cu > 0 ? a.cu : 256);
-  const long long wgs = (ntiles + 3) / 4 < slots ? (ntiles + 3) / 4 : slots;
+  // zero-mean: one workgroup per tile up to the slot count (tiles beyond whole rounds of 4 waves are
+  // worked cooperatively by a workgroup's four waves); with means: one wave per tile
+  const long long want = HM ? (ntiles + 3) / 4 : ntiles;
+  const long long wgs = want < slots ? want : slots;
   hipLaunchKernelGGL((k_fft_wave<N, OUT, HM, CIRC>), dim3((unsigned)wgs), dim3(256), lds, st, a.B, ntiles, lg1, lg2,
                      a.Kp, a.y, a.pr, a.pur, a.pui, a.pc, a.pw, a.pbr, a.pbi, a.h, a.om, a.os, a.oa);
   return hipGetLastError();
