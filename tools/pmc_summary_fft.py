@@ -9,7 +9,7 @@ import os
 import sys
 
 base = sys.argv[1]
-pat = sys.argv[2] if len(sys.argv) > 2 else "k_fft_mfma"
+pat = sys.argv[2] if len(sys.argv) > 2 else "k_fft_"
 
 
 def load(name):
