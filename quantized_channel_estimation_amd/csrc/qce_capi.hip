@@ -927,10 +927,15 @@ namespace {
 
 // memcpy split over a few host threads (pageable numpy buffer <-> pinned slot)
 void par_memcpy(void* dst, const void* src, size_t bytes) {
-  const size_t piece = (size_t)4 << 20;
+  const size_t piece = (size_t)2 << 20;
   int nt = (int)((bytes + piece - 1) / piece);
-  const int hw = (int)std::thread::hardware_concurrency();
-  const int cap = hw >= 16 ? 8 : (hw >= 4 ? hw / 2 : 1);
+  static const int cap = [] {  // QCE_HOST_THREADS (default 16: the CPU share of one GPU on an 8-GPU node)
+    const char* v = getenv("QCE_HOST_THREADS");
+    const int hw = (int)std::thread::hardware_concurrency();
+    int c = v ? atoi(v) : 16;
+    if (hw > 0 && c > hw) c = hw;
+    return c < 1 ? 1 : c;
+  }();
   if (nt > cap) nt = cap;
   if (nt <= 1) {
     memcpy(dst, src, bytes);
@@ -954,7 +959,12 @@ long long host_chunk_rows(const qce_model* m, long long B) {
   if (e && e[0] == '0') return 0;
   const long long width = m->M > m->N ? m->M : m->N;
   long long cap = ((long long)32 << 20) / (16 * width);  // <= 32 MB per slot and direction
-  long long c = (B + 3) / 4;
+  static const long long parts = [] {  // QCE_HOST_CHUNKS: chunks per batch (A/B runs; default 8)
+    const char* v = getenv("QCE_HOST_CHUNKS");
+    const long long n = v ? atoll(v) : 8;
+    return n < 2 ? 2 : n;
+  }();
+  long long c = (B + parts - 1) / parts;
   if (c > cap) c = cap;
   c = (c + 255) / 256 * 256;
   if (c < 4096) c = 4096;
