@@ -61,8 +61,8 @@ typedef struct qce_model qce_model;
 #define QCE_IO_HOST 0
 #define QCE_IO_DEVICE 1
 
+int qce_version(void);
 /* Digest of the sources this library was built from (build.py: sha256 of the csrc .hip / .h files and qce.h). */
-/* Digest of the sources this library was built from (build.py: sha256 of csrc/*.hip, csrc/*.h, qce.h). */
 const char* qce_build_id(void);
 const char* qce_last_error(void);
 int qce_device_count(int* count);
