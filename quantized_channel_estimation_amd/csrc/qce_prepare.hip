@@ -385,9 +385,19 @@ __global__ __launch_bounds__(64) void k_chol_inv_wave(int M, const double2* __re
   __shared__ double dg[64];
   const int k = blockIdx.x, lane = threadIdx.x;
   const double2* src = Cr + (long long)k * M * M;
-  for (int e = lane; e < M * M; e += 64) {
-    const int r = e / M, c = e % M;
-    a[r * LD + c] = src[e];
+  // 16 loads in flight per lane per round (a plain loop waits for each load before its LDS store)
+  for (int base = 0; base < M * M; base += 64 * 16) {
+    double2 v16[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = base + lane + 64 * i;
+      v16[i] = e < M * M ? src[e] : make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = base + lane + 64 * i;
+      if (e < M * M) a[(e / M) * LD + e % M] = v16[i];
+    }
   }
   __syncthreads();
   const int r = lane;
