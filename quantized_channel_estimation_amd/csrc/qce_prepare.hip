@@ -14,6 +14,8 @@
 //   q0_k = Linv_k mu_y,k ; b_k = mu_k - W_k mu_y,k              (:331-332, algebraic form)
 // and packs the FP32 / FP64 fragment-ordered component tables the estimate
 // kernels stream (qce_estimate.hip).
+#include <string.h>
+#include <stdlib.h>
 #include "qce_common.h"
 #include "qce_kernels.h"
 
@@ -683,7 +685,19 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
   hipLaunchKernelGGL(k_gain_cr, dim3(K), dim3(256), 0, st, M, N, p.Cy, p.Cr, p.gain, p.A, p.means, p.means_y, p.Aeff,
                      p.kind, p.n_bits, p.quant_kind, p.delta, p.thr, p.lab, p.beta_first);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  if (M <= 64) {
+  // M <= 64: QCE_CHOL = lds (default) | tri | wave picks the factorisation kernel (A/B runs; metric config,
+  // rocprof: lds 116 us, tri<64> 144 us, one-wave 187 us per prepare of 128 components)
+  static const int chol64 = [] {
+    const char* v = getenv("QCE_CHOL");
+    if (v && strcmp(v, "wave") == 0) return 0;
+    if (v && strcmp(v, "tri") == 0) return 2;
+    return 1;
+  }();
+  if (M <= 64 && chol64 == 1) {
+    hipLaunchKernelGGL(k_chol_inv_lds, dim3(K), dim3(256), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
+  } else if (M <= 64 && chol64 == 2) {
+    hipLaunchKernelGGL(k_chol_inv_tri<64>, dim3(K), dim3(256), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
+  } else if (M <= 64) {
     hipLaunchKernelGGL(k_chol_inv_wave, dim3(K), dim3(64), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
   } else if (M <= 128) {
     hipLaunchKernelGGL(k_chol_inv_tri<128>, dim3(K), dim3(256), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
