@@ -76,8 +76,9 @@ def parse():
     ap.add_argument("--launch-check", action="store_true",
                     help="CPU rehearsal of the launcher: ranks rendezvous over gloo, barrier + MAX-over-ranks "
                          "timing, rank 0 prints one JSON line; no GPU is touched")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic_metric.json"),
-                    help="JSON with PMC-derived HBM bytes per launch of the estimate kernel")
+    ap.add_argument("--traffic", default=None,
+                    help="JSON with PMC-derived HBM bytes per launch of the estimate kernel "
+                         "(default profiles/traffic_<config>.json)")
     a = ap.parse_args()
     if a.shard is None:
         a.shard = DEFAULT_SHARD[a.config]
@@ -482,9 +483,10 @@ def main():
     k_local = (lambda s: s[1] - s[0])(component_slices(K, world)[rank]) if kshard else K
     kern_tag = "fft" if dm.structure()[2] else ("f64" if dtype_of(dm) == "f64" else "h2")
     traffic = None
-    if os.path.exists(args.traffic):
+    tpath = args.traffic or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    if os.path.exists(tpath):
         try:
-            tj = json.load(open(args.traffic))
+            tj = json.load(open(tpath))
             if tj.get("config") == args.config and tj.get("B") == B and tj.get("kernel") == kern_tag:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
