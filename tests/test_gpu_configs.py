@@ -102,3 +102,24 @@ def test_bench_kshard_two_ranks_gloo_one_gpu():
     d = json.loads(line[-1])
     assert d["world_size"] == 2 and d["config"]["shard"] == "k" and d["dtype"] == "f64"
     assert d["parity"]["rel_fro"] < 1e-9
+
+
+@pytest.mark.gpu
+def test_size_limits():
+    """Shape limits of the C ABI: N > 256 is refused at model creation, the selective modes take K <= 256
+    (QCE_ENOTIMPL -> NotImplementedError), while 'all' mode runs any K (here 300, vs the FP64 oracle)."""
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import _lib, inputs
+    means, covs, w = inputs.synthetic_model(300, 16, seed=9)
+    rng = np.random.default_rng(9)
+    y = (np.sign(rng.standard_normal((40, 16))) + 1j * np.sign(rng.standard_normal((40, 16)))) / np.sqrt(2)
+    dm = _lib.DeviceModel(means, covs, w)
+    dm.prepare(None, 5.0, 1.0)
+    h = dm.estimate(y)
+    assert rel_fro(h, O.estimate(means, covs, w, y, 5.0, 16, None, "all", 1)) < 1e-9
+    with pytest.raises(NotImplementedError):
+        dm.estimate(y, _lib.MODE_TOPN, 1.0)
+    dm.close()
+    big = np.eye(257)[None].astype(complex)
+    with pytest.raises(NotImplementedError):
+        _lib.DeviceModel(None, big, np.ones(1))
