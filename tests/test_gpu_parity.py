@@ -439,3 +439,44 @@ def test_fourier_mfma_kernel_vs_lds_kernel(K, N, blocks, B, n_bits, mean, monkey
     assert rel_fro(out["mfma"][0], ho) < tol
     assert rel_fro(out["mfma"][0], out["lds"][0]) < 1e-12
     assert rel_fro(out["mfma"][1], ho) < 1e-6  # partial acc is fp32
+
+
+@pytest.mark.parametrize("K,N,blocks,B,n_bits,qtype,mean", [
+    (128, 64, None, 70013, 3, "lloyd", False),   # cfg3 geometry: two whole rounds of tiles + a ragged tail
+    (64, 64, (8, 8), 70013, 1, "uniform", False),  # 2-D transform through the same phases
+    (16, 16, (4, 4), 40013, 2, "uniform", False),
+    (32, 32, None, 20013, np.inf, "uniform", True),  # with means: every tile one wave, persistent loop
+])
+def test_fourier_wave_kernel_persistent_phases(K, N, blocks, B, n_bits, qtype, mean, monkeypatch):
+    """k_fft_wave (N <= 64) at batches large enough for its main phase: one wave per 16-row tile over
+    whole rounds of the persistent grid, with the next tile's y prefetched behind the current one, then
+    the remainder worked cooperatively by the four waves of a workgroup (zero-mean models).  Small-batch
+    tests reach only the cooperative phase.  One launch (QCE_HOST_PIPELINE=0); rows from the first
+    round, the main/tail boundary and the ragged end are checked against the FP64 oracle, and the first
+    rows against the same rows estimated alone (cooperative phase), to FP64 rounding."""
+    _gpu_or_skip()
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import Gmm_nbit, inputs
+    monkeypatch.setenv("QCE_HOST_PIPELINE", "0")
+    cov = "circulant" if blocks is None else "block-circulant"
+    means, covs, w = inputs.synthetic_model(K, N, cov_type=cov, seed=K + N, blocks=blocks)
+    rng = np.random.default_rng(B)
+    if mean:
+        means = 0.3 * inputs.crandn(K, N, rng=rng)
+    h = inputs.crandn(B, N, rng=rng)
+    qz = (None, None, None)
+    if n_bits not in (1, np.inf):
+        qz = inputs.get_quantizer([5.0], n_bits, qtype)[5.0]
+    y = inputs.get_observation_nbit(h, 5.0, None, n_bits, qz[0], qz[1], rng=rng)
+    g = Gmm_nbit.from_params(means, covs, w)
+    hg = g.estimate_from_y(y, 5.0, N, None, "all", n_bits, qtype, qz)
+    assert g._dev.structure()[2] == 1
+    assert hg.shape == (B, N) and np.isfinite(hg).all()
+    tol = 1e-9 if n_bits != 1 else 1e-7
+    ntiles = (B + 15) // 16
+    edge = (ntiles // 2048) * 2048 * 16  # main/tail boundary at 256 CUs x 2 workgroups x 4 waves
+    for lo, hi in ((0, 200), (max(edge - 100, 0), edge + 100), (B - 200, B)):
+        ho = O.estimate(means, covs, w, y[lo:hi], 5.0, N, None, "all", n_bits, qtype, qz)
+        assert rel_fro(hg[lo:hi], ho) < tol, (lo, hi, rel_fro(hg[lo:hi], ho))
+    alone = g.estimate_from_y(y[:300], 5.0, N, None, "all", n_bits, qtype, qz)
+    assert rel_fro(hg[:300], alone) < 1e-12
