@@ -249,6 +249,11 @@ def f64_executed_flops(N, K, B):
     return 256.0 * (ntl * (ntl + 1) + ntw * kp) * K * B
 
 
+def dm_has_mean(dm):
+    """Whether the device model carries non-zero means (the bench's synthetic models are zero-mean)."""
+    return bool(getattr(dm, "has_mean", False))
+
+
 def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
     N = cfg["N"]
     fourier = bool(dm.structure()[2])
@@ -267,18 +272,31 @@ def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
                     fp64_frac=round(fft_flops / (kern_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
                     note="HBM roofline per SURVEY D3 (32 N B per estimate); the kernel's binding resource is FP64 "
                          "issue (4 K N MFMA + FFT VALU flops per estimate), reported as fp64_frac")
-    flops = 16.0 * k_local * N * N * B  # 16 K M N real flops per estimate
+    M = N  # A = I at every bench config (n_pilots = 1)
+    flops = 16.0 * k_local * N * N * B  # 16 K M N real flops per estimate (dense count)
+    if dm.precision == "f64":
+        # minimal useful work per (sample, component): the triangular quad form ||Linv y||^2 = M(M+1)/2 complex
+        # MACs (4 M (M+1) real flops) + the filter W y = M N complex MACs (8 M N); with a mean model the -q0
+        # and b columns add 8 M + 8 N.  This is what the kernel has to do, so frac = useful / time / peak <= 1.
+        useful_per = 4.0 * M * (M + 1) + 8.0 * M * N + (8.0 * (M + N) if dm_has_mean(dm) else 0.0)
+        useful = useful_per * k_local * B
+        achieved = useful / (kern_ms * 1e-3) / 1e12
+        frac = achieved / FP64_MFMA_PEAK_TFLOPS
+        assert frac <= 1.0, f"roofline frac {frac:.4f} > 1: the useful-work count or the kernel timing is wrong"
+        kernel = "k_est_all_f64 (+k_merge_f64)" if N <= 128 else "k_lp_f64 + k_select + k_wsum_f64"
+        line = dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
+                    frac=round(frac, 4), traffic=traffic, kernel=kernel, peak_dtype="fp64 MFMA (dense)",
+                    kernel_ms=round(kern_ms, 4), useful_flops_per_estimate_component=useful_per,
+                    flops_per_launch=useful, dense_16KMN_flops_per_launch=flops,
+                    note="frac = minimal useful flops (4M(M+1) triangular quad form + 8MN filter per sample and "
+                         "component) / kernel time / FP64 MFMA peak; mfma_issue_frac = executed MFMA flops / "
+                         "time / peak (the pipe occupancy, includes the padding of the 16x16 tiles)")
+        if N <= 128:
+            ex = f64_executed_flops(N, k_local, B)
+            line["executed_flops_per_launch"] = ex
+            line["mfma_issue_frac"] = round(ex / (kern_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4)
+        return line
     achieved = flops / (kern_ms * 1e-3) / 1e12
-    if dm.precision == "f64" and N <= 128:
-        ex = f64_executed_flops(N, k_local, B)
-        return dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
-                    frac=round(achieved / FP64_MFMA_PEAK_TFLOPS, 4), traffic=traffic,
-                    kernel="k_est_all_f64 (+k_merge_f64)", peak_dtype="fp64 MFMA (dense)",
-                    kernel_ms=round(kern_ms, 4), flops_per_launch=flops, executed_flops_per_launch=ex,
-                    mfma_issue_frac=round(ex / (kern_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
-                    note="algorithmic flops (16KMN) / time; frac can exceed 1 because the upper triangle of "
-                         "Linv is skipped (executed = %.3f of algorithmic here): mfma_issue_frac is the "
-                         "executed-MFMA fraction of the FP64 peak" % (ex / flops))
     nsl = (2 * N) // 32
     tri = (sum(2 * r + 2 for r in range(nsl)) / (nsl * 2 * nsl) + 1.0) / 2.0
     ex = flops * tri * 2.0

@@ -160,6 +160,7 @@ class DeviceModel:
         self.K, self.N, self.device = K, N, int(device)
         self.M = 0
         self.precision = "f64"
+        self.has_mean = bool(means is not None and np.any(means != 0))
 
     @property
     def handle(self):
@@ -175,6 +176,7 @@ class DeviceModel:
         w = np.ascontiguousarray(weights, dtype=np.float64).reshape(self.K)
         check(load().qce_model_set_params(self._h, ptr(means), ptr(covs), ptr(w)))
         self.M = 0
+        self.has_mean = bool(means is not None and np.any(means != 0))
 
     def close(self):
         if getattr(self, "_h", None):
