@@ -66,7 +66,8 @@ def parse():
     ap.add_argument("--shard", default=None, choices=["batch", "k"])
     ap.add_argument("--precision", default="f64", choices=["f64", "fast"],
                     help="dense 'all' arithmetic: f64 (the reference's complex128, default) or fast (fp16 split)")
-    ap.add_argument("--chunks", type=int, default=4, help="K-shard pipeline chunks per batch")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="K-shard pipeline chunks per batch (0 = sharding.default_chunks: 4, or 8 from 4 ranks on)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--collective", default="rs", choices=["rs", "ar"],
                     help="K-shard SUM collective: reduce-scatter (rank keeps its rows) or all-reduce")
@@ -375,7 +376,7 @@ def main():
     import torch
     import torch.distributed as dist
     from quantized_channel_estimation_amd import _lib
-    from quantized_channel_estimation_amd.sharding import ComponentShardEstimator, component_slices
+    from quantized_channel_estimation_amd.sharding import ComponentShardEstimator, component_slices, default_chunks
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -447,7 +448,8 @@ def main():
                     return r
                 shard.dev.partial_shifted = timed
             try:
-                return shard.estimate(yd, chunks=args.chunks, scatter=args.collective == "rs")
+                # no host sync inside a step: the flag word is read once per timed region (shard.finish)
+                return shard.estimate(yd, chunks=args.chunks or None, scatter=args.collective == "rs", sync=False)
             finally:
                 shard.dev.partial_shifted = orig
 
@@ -456,8 +458,13 @@ def main():
         if world > 1:
             dist.barrier()
 
+    def finish(res):
+        # K-shard: the natural sync point of a run of steps -- Cholesky failures raise, flagged rows are recombined
+        return shard.finish() if kshard else res
+
     for _ in range(args.warmup):
-        step()
+        res = step()
+    finish(res)
     barrier()
     if kshard:
         events = [[] for _ in range(args.steps)]  # filled per chunk by the timed partial launches
@@ -467,6 +474,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         res = step(events[i])
+    res = finish(res)
     barrier()
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([sum(a.elapsed_time(b) for a, b in evs) for evs in events]))
@@ -537,7 +545,7 @@ def main():
                                    f"{'' if args.shard == 'k' else '/GPU'} prepare-per-step",
                        "K": K, "N": N, "B": B, "shard": args.shard,
                        "parallelism": f"{'kshard' if args.shard == 'k' else 'batch'}{world}",
-                       "chunks": args.chunks if kshard else None},
+                       "chunks": (args.chunks or default_chunks(world)) if kshard else None},
             "mse": mse,
             "parity": parity,
             "roofline": roofline,

@@ -80,11 +80,15 @@ int qce_model_set_params(qce_model* model, const double* means_cplx, const doubl
 
 /* Per-SNR precompute: `_prepare_for_prediction` (gmm_cplx_bussgang.py:246-328).
  * A: (M,N) c128 observation matrix, or NULL for the identity (estimate_from_y :191-192).
- * n_bits: 1..8 or +INFINITY (np.inf).  thresholds (2^b-1) / labels (2^b) are the quantiser
- * tables of the lloyd kind (lloyd_max_quantizer.py:24-37); NULL otherwise.
- * Runs on `stream` (NULL = the model's stream; pass the stream later estimates use so a prepare never
- * overwrites tables an in-flight estimate still reads) and synchronises it to read the Cholesky status.
- * Returns QCE_ECHOL if some Cr_k is not positive definite (:43-46). */
+ * n_bits: 1..16 (uniform; beyond 8 bits the step is the reference's asymptote 4 sqrt(b) 2^-b,
+ * uniform_quantizer.py:15-21; lloyd: 1..8) or +INFINITY (np.inf).  thresholds (2^b-1) / labels (2^b) are the
+ * quantiser tables of the lloyd kind (lloyd_max_quantizer.py:24-37); NULL otherwise.
+ * Runs asynchronously on `stream` (NULL = the model's stream; pass the stream later estimates use so a prepare
+ * never overwrites tables an in-flight estimate still reads); no host synchronisation.  The per-component
+ * Cholesky status is copied behind the prepare's kernels and read at the next call that synchronises anyway
+ * (host-I/O estimates, qce_log_prob, qce_get_tables, qce_synchronize, host-I/O qce_cconst_max), which returns
+ * QCE_ECHOL if some Cr_k is not positive definite (:43-46).  Device-I/O estimates issued in between compute on
+ * NaN tables; device-I/O callers read the status through qce_cconst_max (it writes +inf on a failure). */
 int qce_prepare(qce_model* model, const double* A, int M, double snr_db, double n_bits, int quant_kind,
                 const double* thresholds, const double* labels, int n_levels, void* stream);
 
@@ -119,7 +123,10 @@ int qce_estimate_partial_shifted(qce_model* model, const double* y, int64_t B, c
                                  int io, void* stream);
 
 /* out[0] = max_k cconst_k of the last prepare (this shard's part of the shift above; the caller reduces it over
- * shards with a MAX collective).  `out` where `io` says; device I/O is asynchronous on `stream`. */
+ * shards with a MAX collective), or +INFINITY if the prepare's Cholesky factorisation failed for some component:
+ * the failure then travels with the shift through the MAX collective to every shard (sharding.py raises the
+ * reference's ValueError).  `out` where `io` says; device I/O is asynchronous on `stream`, host I/O synchronises
+ * and returns QCE_ECHOL on a failure. */
 int qce_cconst_max(qce_model* model, double* out, int io, void* stream);
 
 /* Per-SNR tables for state mirroring (the reference mutates gm.means_, gm.covariances_,

@@ -19,6 +19,13 @@ PRECISION_F64, PRECISION_FAST = 0, 1
 QUANT_UNIFORM, QUANT_LLOYD, QUANT_OTHER = 0, 1, 2
 IO_HOST, IO_DEVICE = 0, 1
 
+# The reference's message for a non-positive-definite Cr_k (gmm_cplx_bussgang.py:33-37, raised at :43-46); the
+# library returns the same text with QCE_ECHOL (csrc/qce_capi.hip check_status), the K-shard path raises it from
+# the flag its shift carries (sharding.py).
+CHOL_MESSAGE = ("Fitting the mixture model failed because some components have ill-defined empirical covariance "
+                "(for instance caused by singleton or collapsed samples). Try to decrease the number of "
+                "components, or increase reg_covar.")
+
 _c_dbl_p = ctypes.POINTER(ctypes.c_double)
 _c_flt_p = ctypes.POINTER(ctypes.c_float)
 _c_i64_p = ctypes.POINTER(ctypes.c_int64)

@@ -456,6 +456,14 @@ bool fft_mfma_enabled() {
   return !(e && strcmp(e, "lds") == 0);
 }
 
+// Uniform quantiser step get_uniform_quant_step (uniform_quantizer.py:44-45) with standard_quantization_step
+// (:6-23): J. Max's table for n_bits <= 8, the asymptote 4 sqrt(b) 2^-b of Hui & Neuhoff beyond it (:15-21).
+double uniform_step(double snr_db, int nb) {
+  static const double tbl[9] = {0, 1.596, 0.9957, 0.5860, 0.3352, 0.1881, 0.1041, 0.0569, 0.0308};
+  const double std_step = nb <= 8 ? tbl[nb] : 4.0 * sqrt((double)nb) * pow(2.0, -nb);
+  return sqrt((1.0 + pow(10.0, -snr_db / 10.0)) / 2.0) * std_step;
+}
+
 // The Cholesky status of a prepare is copied to pinned host memory behind the prepare's kernels and read only
 // when a call synchronises anyway (host I/O, qce_synchronize, qce_get_tables): a prepare costs no host round
 // trip.  A failed prepare surfaces as QCE_ECHOL there (device-I/O estimates in between compute on NaN tables).
@@ -653,11 +661,11 @@ int qce_prepare(qce_model* m, const double* A, int M, double snr_db, double n_bi
 namespace {
 // The dense tables of a prepare that took the Fourier path, computed when first asked for
 // (qce_get_tables: the reference's gm state mirror); the Fourier tables stay active.
-int ensure_dense(qce_model* m) {
+int ensure_dense(qce_model* m, void* stream = nullptr) {
   if (!m->fft_active || m->dense_valid) return QCE_OK;
   const int rc = prepare_impl(m, nullptr, m->last.M, m->last.snr_db, m->last.n_bits, m->last.quant_kind,
                               m->last.thr.empty() ? nullptr : m->last.thr.data(),
-                              m->last.lab.empty() ? nullptr : m->last.lab.data(), m->last.n_levels, nullptr, false);
+                              m->last.lab.empty() ? nullptr : m->last.lab.data(), m->last.n_levels, stream, false);
   if (rc) return rc;
   m->fft_active = 1;
   m->dense_valid = 1;
@@ -682,10 +690,11 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
   } else if (isinf(n_bits) && n_bits > 0) {
     kind = 2;
   } else {
-    if (!(n_bits >= 2.0 && n_bits <= 8.0) || n_bits != floor(n_bits))
-      return fail(QCE_ENOTIMPL, "n_bits must be 1..8 or inf");
+    if (!(n_bits >= 2.0 && n_bits <= (double)QCE_MAX_UNIFORM_BITS) || n_bits != floor(n_bits))
+      return fail(QCE_ENOTIMPL, "n_bits must be 1.." + std::to_string(QCE_MAX_UNIFORM_BITS) + " or inf");
     kind = 1;
     nb = (int)n_bits;
+    if (quant_kind == QCE_QUANT_LLOYD && nb > 8) return fail(QCE_ENOTIMPL, "lloyd quantiser tables cover n_bits <= 8");
   }
   if (kind == 1 && quant_kind == QCE_QUANT_LLOYD) {
     if (!thresholds || !labels || n_levels != (1 << nb))
@@ -727,10 +736,7 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
     HIPCHK(m->thr.ensure(256));
     HIPCHK(m->lab.ensure(256));
     double delta = 0.0;
-    if (kind == 1 && quant_kind == QCE_QUANT_UNIFORM) {
-      static const double tbl[9] = {0, 1.596, 0.9957, 0.5860, 0.3352, 0.1881, 0.1041, 0.0569, 0.0308};
-      delta = sqrt((1.0 + pow(10.0, -snr_db / 10.0)) / 2.0) * tbl[nb];
-    }
+    if (kind == 1 && quant_kind == QCE_QUANT_UNIFORM) delta = uniform_step(snr_db, nb);
     if (kind == 1 && quant_kind == QCE_QUANT_LLOYD) {
       HIPCHK(hipMemcpyAsync(m->thr.p, thresholds, sizeof(double) * (n_levels - 1), hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(m->lab.p, labels, sizeof(double) * n_levels, hipMemcpyHostToDevice, st));
@@ -837,11 +843,7 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
       }
   }
   double delta = 0.0;
-  if (kind == 1 && quant_kind == QCE_QUANT_UNIFORM) {
-    // uniform_quantizer.py:6-23, 44-45
-    static const double tbl[9] = {0, 1.596, 0.9957, 0.5860, 0.3352, 0.1881, 0.1041, 0.0569, 0.0308};
-    delta = sqrt((1.0 + pow(10.0, -snr_db / 10.0)) / 2.0) * tbl[nb];
-  }
+  if (kind == 1 && quant_kind == QCE_QUANT_UNIFORM) delta = uniform_step(snr_db, nb);
   if (kind == 1 && quant_kind == QCE_QUANT_LLOYD) {
     HIPCHK(hipMemcpyAsync(m->thr.p, thresholds, sizeof(double) * (n_levels - 1), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(m->lab.p, labels, sizeof(double) * n_levels, hipMemcpyHostToDevice, st));
@@ -1312,14 +1314,14 @@ int qce_cconst_max(qce_model* m, double* out, int io, void* stream) {
   if (!out) return fail(QCE_EARG, "null out");
   DeviceGuard g(m->device);
   hipStream_t st = pick_stream(m, stream);
-  if (m->fft_active && (rc = ensure_dense(m))) return rc;
+  if (m->fft_active && (rc = ensure_dense(m, st))) return rc;
   if (io == QCE_IO_HOST) {
     HIPCHK(m->shift_scr.ensure(1));
-    HIPCHK(qce_launch_cconst_max(m->K, m->cconst.p, m->shift_scr.p, st));
+    HIPCHK(qce_launch_cconst_max(m->K, m->cconst.p, m->status.p, m->shift_scr.p, st));
     HIPCHK(hipMemcpyAsync(out, m->shift_scr.p, sizeof(double), hipMemcpyDeviceToHost, st));
     HOST_SYNC_CHECK(m, st);
   } else {
-    HIPCHK(qce_launch_cconst_max(m->K, m->cconst.p, out, st));
+    HIPCHK(qce_launch_cconst_max(m->K, m->cconst.p, m->status.p, out, st));
   }
   return QCE_OK;
 }

@@ -4,6 +4,8 @@
 #include <stdint.h>
 
 #define QCE_DEV __device__ __forceinline__
+// widest uniform quantiser qce_prepare accepts (the Bussgang gain sums 2^b - 1 terms per diagonal entry)
+#define QCE_MAX_UNIFORM_BITS 16
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));

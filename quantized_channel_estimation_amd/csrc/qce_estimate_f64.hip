@@ -196,10 +196,14 @@ hipError_t qce_launch_f32_to_f64(const float* a, double* b, long long n, hipStre
   return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void k_cconst_max(int K, const double* __restrict__ c, double* __restrict__ out) {
+// out[0] = max_k c_k, or +inf when the prepare left a non-zero Cholesky status for some component: the flag rides
+// the shard shift through its MAX collective, so every rank learns of a failed factorisation on any rank without a
+// host round trip (sharding.py raises the reference's ValueError, gmm_cplx_bussgang.py:43-46).
+__global__ __launch_bounds__(256) void k_cconst_max(int K, const double* __restrict__ c, const int* __restrict__ status,
+                                                    double* __restrict__ out) {
   __shared__ double red[256];
   double v = -__builtin_inf();
-  for (int k = threadIdx.x; k < K; k += 256) v = fmax(v, c[k]);
+  for (int k = threadIdx.x; k < K; k += 256) v = fmax(v, (status && status[k]) ? __builtin_inf() : c[k]);
   red[threadIdx.x] = v;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
@@ -208,7 +212,7 @@ __global__ __launch_bounds__(256) void k_cconst_max(int K, const double* __restr
   }
   if (threadIdx.x == 0) out[0] = red[0];
 }
-hipError_t qce_launch_cconst_max(int K, const double* cconst, double* out, hipStream_t st) {
-  hipLaunchKernelGGL(k_cconst_max, dim3(1), dim3(256), 0, st, K, cconst, out);
+hipError_t qce_launch_cconst_max(int K, const double* cconst, const int* status, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_cconst_max, dim3(1), dim3(256), 0, st, K, cconst, status, out);
   return hipGetLastError();
 }

@@ -113,7 +113,7 @@ hipError_t qce_launch_est_f64(const QceF64Args& a, bool out_partial, hipStream_t
 hipError_t qce_launch_pack_shifted(long long B, int N, const double* m, const double* s, const double* acc,
                                    const float* acc32, const double* shift, double* pk, hipStream_t st);
 // out[0] = max_k cconst[k] (device), the local part of the K-shard shift M*
-hipError_t qce_launch_cconst_max(int K, const double* cconst, double* out, hipStream_t st);
+hipError_t qce_launch_cconst_max(int K, const double* cconst, const int* status, double* out, hipStream_t st);
 hipError_t qce_launch_f64_to_f32(const double* a, float* b, long long n, hipStream_t st);
 hipError_t qce_launch_f32_to_f64(const float* a, double* b, long long n, hipStream_t st);
 

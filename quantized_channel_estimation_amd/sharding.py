@@ -11,17 +11,25 @@ here one SNR point's batch is split over the GPUs of a node, two ways (SURVEY.md
   SUM collective of these (B, 2N+2) rows gives h_b = acc / s.  The batch is cut into chunks; chunk
   i's collective (reduce-scatter by default: each rank keeps its slice of the rows, half the bytes
   of an all-reduce) is issued asynchronously and runs on RCCL's stream while chunk i+1's partial
-  kernel runs on the compute stream.  Rows whose sum underflows everywhere (min quad form > ~700
-  above M*) are detected with one small all-reduce per step and recombined exactly (MAX of m, then
-  SUM).
+  kernel runs on the compute stream.  Rows whose shifted sum leaves the normal FP64 range (max lp more
+  than ~667 below M*) are flagged on the device; one tiny MAX all-reduce per step agrees on a flag word
+  (flagged rows, Cholesky failure on any rank) that the host reads once at the caller's sync point
+  (``finish``), and only the flagged rows are recombined exactly (MAX of m, then SUM).  The collectives
+  per step: the per-chunk SUM (reduce-scatter) and the 2-double flag MAX; per SNR point: the shift MAX.
 * **batch shards** (``BatchShardEstimator``): every rank holds the whole mixture and estimates a
   disjoint slice of the observations.  No data-path collective — the samples are independent (the
   configuration for the HBM-bound Fourier paths, where a K-shard collective costs more than the
   kernel).
 """
+import math
+
 import numpy as np
 
 from . import _lib
+
+# A row whose shifted sum falls below this is recombined exactly: above it every term that matters is a normal
+# double (DBL_MIN = 2.2e-308), so the shifted sums carry full FP64 precision.
+UNDERFLOW_S = 1e-290
 
 
 def combine_partials_numpy(parts, N):
@@ -73,7 +81,7 @@ def combine_partials_dist(m, s, acc, shift, N, group=None):
     buf[:, 0] = s * sc
     buf[:, 1:] = acc.to(torch.float64) * sc[:, None]
     dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
-    bad = buf[:, 0] == 0
+    bad = buf[:, 0] < UNDERFLOW_S
     nbad = bad.sum()
     dist.all_reduce(nbad, op=dist.ReduceOp.MAX, group=group)  # tiny: agree on the fallback
     if int(nbad.item()) > 0:
@@ -112,8 +120,20 @@ def _packed_to_complex(rows):
     return torch.complex(acc[:, 0::2].contiguous(), acc[:, 1::2].contiguous())
 
 
+def default_chunks(world):
+    """Pipeline chunks per batch: 4, or 8 from four ranks on (the per-chunk collective shrinks with the rank
+    count, so more chunks keep the exposed last-chunk share small)."""
+    return 8 if world >= 4 else 4
+
+
 class ComponentShardEstimator:
-    """K-sharded 'all'-mode estimator: this rank's slice of the mixture on its own GPU."""
+    """K-sharded 'all'-mode estimator: this rank's slice of the mixture on its own GPU.
+
+    Per step the host enqueues the chunk kernels and collectives and one tiny MAX all-reduce of a flag word
+    [rows whose shifted sum underflowed, Cholesky failure on any rank]; with ``sync=False`` it returns without
+    waiting for the device, and ``finish()`` (the caller's natural sync point) reads the flag word once, raises the
+    reference's ValueError for a failed factorisation (gmm_cplx_bussgang.py:43-46) and recombines the flagged rows
+    exactly.  ``sync=True`` (default) is estimate + finish."""
 
     def __init__(self, means_cplx, covs_cplx, weights, rank, world, device=0, group=None, precision="f64"):
         K = np.asarray(covs_cplx).shape[0]
@@ -128,38 +148,57 @@ class ComponentShardEstimator:
         self.group = group
         self.shift = None
         self._bufs = {}
+        self._pending = None
+        self._flag_acc = None
+
+    def _on_gpu(self):
+        return getattr(self.dev, "device_type", "cuda") == "cuda"
 
     def prepare(self, A, snr_db, n_bits, quant_kind=_lib.QUANT_UNIFORM, thresholds=None, labels=None, stream=None):
-        """Per-rank prepare of its components and the common shift M* (one scalar MAX all-reduce).  On the GPU
-        the shift stays on the device: this rank's max c_k is written by a kernel on torch's current stream and
-        all-reduced there, and the partial kernels read it — no host round trip per SNR point."""
+        """Per-rank prepare of its components and the common shift M* (one scalar MAX all-reduce).  The shift stays
+        on the device: this rank's max c_k (+inf if one of its Cholesky factorisations failed) is written by a kernel
+        on the prepare's stream, and the all-reduce is ordered behind it -- no host round trip per SNR point."""
         import torch
         import torch.distributed as dist
-        dev = torch.device("cuda", self.dev.device)
-        cur = torch.cuda.current_stream(dev)
-        self.dev.prepare(A, snr_db, n_bits, quant_kind, thresholds, labels,
-                         stream=stream if stream is not None else cur.cuda_stream)
-        if not isinstance(self.shift, torch.Tensor):
+        if self._on_gpu():
+            dev = torch.device("cuda", self.dev.device)
+            cur = torch.cuda.current_stream(dev)
+            s = stream if stream is not None else cur.cuda_stream
+        else:
+            dev, cur, s = torch.device("cpu"), None, None
+        self.dev.prepare(A, snr_db, n_bits, quant_kind, thresholds, labels, stream=s)
+        if not isinstance(self.shift, torch.Tensor) or self.shift.device != dev:
             self.shift = torch.empty(1, dtype=torch.float64, device=dev)
-        self.dev.cconst_max(out=self.shift, stream=cur.cuda_stream)
+        self.dev.cconst_max(out=self.shift, stream=s)
+        if cur is not None and s != cur.cuda_stream:  # the collective runs behind torch's current stream
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.ExternalStream(s, device=dev))
+            cur.wait_event(ev)
         if self.world > 1:
             dist.all_reduce(self.shift, op=dist.ReduceOp.MAX, group=self.group)
 
     def _buf(self, key, shape, device):
         import torch
         b = self._bufs.get(key)
-        if b is None or tuple(b.shape) != tuple(shape):
+        if b is None or tuple(b.shape) != tuple(shape) or b.device != device:
             b = torch.empty(shape, dtype=torch.float64, device=device)
             self._bufs[key] = b
         return b
 
-    def estimate(self, y, chunks=4, scatter=True):
-        """'all'-mode estimates of y (B, M) complex128 CUDA tensor.
+    def _chol_flag(self, device):
+        import torch
+        if isinstance(self.shift, torch.Tensor):
+            return torch.isinf(self.shift).to(torch.float64).reshape(1)
+        return torch.tensor([1.0 if math.isinf(float(self.shift)) else 0.0], dtype=torch.float64, device=device)
+
+    def estimate(self, y, chunks=None, scatter=True, sync=True):
+        """'all'-mode estimates of y (B, M) complex128 tensor.
 
         scatter=True: reduce-scatter per chunk, returns (rows, h) with h (n, N) complex128 the estimates of
         this rank's rows (global row indices `rows`, a LongTensor); scatter=False: all-reduce, every rank
         gets h for all B rows (rows = None).  The partial kernels run on torch's current stream, each
-        chunk's collective asynchronously on RCCL's stream behind it."""
+        chunk's collective asynchronously on RCCL's stream behind it.  sync=False: no host synchronisation; call
+        finish() before reading h (rows whose shifted sum underflowed are NaN until then)."""
         import torch
         import torch.distributed as dist
         B = y.shape[0]
@@ -168,7 +207,7 @@ class ComponentShardEstimator:
         stream = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else None
         multi = self.world > 1
         use_rs = scatter and multi
-        bounds = chunk_bounds(B, chunks, self.world, use_rs)
+        bounds = chunk_bounds(B, default_chunks(self.world) if chunks is None else chunks, self.world, use_rs)
         works, pieces = [], []
         for i, (lo, hi) in enumerate(bounds):
             n = hi - lo
@@ -188,34 +227,71 @@ class ComponentShardEstimator:
                     works.append(dist.all_reduce(pk[:n], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
                 pieces.append((lo, hi, pk[:n]))
         for wk in works:
-            wk.wait()
-        rows = torch.cat([r[:max(0, b - a)] for a, b, r in pieces]) if pieces else None
-        # underflow guard: one tiny collective per step agrees on whether any row summed to s = 0
-        nbad = (rows[:, 0] == 0).sum().to(torch.float64).reshape(1)
+            wk.wait()  # RCCL: the current stream waits on the collective (no host wait)
+        rows = torch.cat([r[:max(0, b - a)] for a, b, r in pieces])
+        # the step's flag word: [rows to recombine exactly, Cholesky failure on some rank], agreed with one MAX
+        bad = rows[:, 0] < UNDERFLOW_S
+        flags = torch.cat([bad.sum().to(torch.float64).reshape(1), self._chol_flag(dev)])
         if multi:
-            dist.all_reduce(nbad, op=dist.ReduceOp.MAX, group=self.group)
-        if float(nbad.item()) > 0:
-            return self._exact(y, use_rs, pieces)
+            dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.group)
+        self._flag_acc = flags if self._flag_acc is None else torch.maximum(self._flag_acc, flags)
         h = _packed_to_complex(rows)
-        if not use_rs:
-            return None, h
-        idx = torch.cat([torch.arange(a, max(a, b), device=dev) for a, b, _ in pieces])
+        idx = torch.cat([torch.arange(a, max(a, b), device=dev) for a, b, _ in pieces]) if use_rs else None
+        self._pending = (y, use_rs, bad, idx, h, flags)
+        if sync:
+            return self.finish()
         return idx, h
 
-    def _exact(self, y, use_rs, pieces):
-        """Rare path: exact two-step combine of the unshifted FP64 partials for the whole batch."""
+    def finish(self):
+        """Read the flag words of the steps since the last finish() (one host sync): raise ValueError with the
+        reference's message if a Cholesky factorisation failed on any rank, recombine the underflowed rows of the
+        latest result exactly (in place) and return it as (rows, h)."""
+        if self._pending is None:
+            return None
+        y, use_rs, bad, idx, h, flags = self._pending
+        acc = self._flag_acc
+        self._pending = self._flag_acc = None
+        f_last, f_any = flags.tolist(), acc.tolist()
+        if f_any[1] > 0:
+            raise ValueError(_lib.CHOL_MESSAGE)
+        if f_any[0] > f_last[0]:
+            raise RuntimeError("an earlier K-shard estimate had rows whose shifted sum underflowed; estimate it "
+                               "with sync=True to have them recombined")
+        if f_last[0] > 0:
+            self._repair(y, use_rs, bad, idx, h)
+        return idx, h
+
+    def _repair(self, y, use_rs, bad, idx, h):
+        """Rare path: exact two-step combine (MAX of m, then SUM) of the unshifted FP64 partials, for the flagged
+        rows only.  Under reduce-scatter every rank flags only rows it owns, so the row set is gathered first."""
         import torch
-        stream = torch.cuda.current_stream(y.device).cuda_stream if y.device.type == "cuda" else None
-        m, s, acc = self.dev.partial64(y, stream=stream)
-        if self.world > 1:
-            h = combine_partials_dist(m, s, acc, self.shift, self.N, self.group)
+        import torch.distributed as dist
+        dev = y.device
+        stream = torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else None
+        mine = torch.nonzero(bad, as_tuple=False).flatten()
+        gmine = idx[mine] if use_rs else mine
+        if use_rs:
+            cnt = torch.tensor([gmine.numel()], dtype=torch.int64, device=dev)
+            dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=self.group)
+            padded = torch.full((int(cnt.item()),), -1, dtype=torch.int64, device=dev)
+            padded[:gmine.numel()] = gmine
+            allv = [torch.empty_like(padded) for _ in range(self.world)]
+            dist.all_gather(allv, padded, group=self.group)
+            grows = torch.unique(torch.cat(allv))
+            grows = grows[grows >= 0]
         else:
-            h = torch.from_numpy(combine_partials_numpy([(m.cpu().numpy(), s.cpu().numpy(), acc.cpu().numpy())],
-                                                        self.N)).to(y.device)
-        if not use_rs:
-            return None, h
-        idx = torch.cat([torch.arange(a, max(a, b), device=y.device) for a, b, _ in pieces])
-        return idx, h[idx]
+            grows = gmine
+        m, s, acc = self.dev.partial64(y[grows], stream=stream)
+        if self.world > 1:
+            hx = combine_partials_dist(m, s, acc, self.shift, self.N, self.group)
+        else:
+            hx = torch.from_numpy(combine_partials_numpy(
+                [(m.cpu().numpy(), s.cpu().numpy(), acc.cpu().numpy())], self.N)).to(dev)
+        if use_rs:  # this rank's flagged rows are a subset of grows (sorted): locate them
+            pos = torch.searchsorted(grows, gmine)
+            h[mine] = hx[pos]
+        else:
+            h[grows] = hx
 
 
 class BatchShardEstimator:

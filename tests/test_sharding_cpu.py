@@ -97,30 +97,38 @@ def test_slices_cover_and_balance():
 # ---- pipelined K-shard estimator (chunked, shifted packed partials, async reduce-scatter / all-reduce) ----
 class _OracleShard:
     """Stand-in for one rank's DeviceModel: the FP64 oracle's partial of components [lo, hi) in the
-    formats qce_estimate_partial_shifted / qce_estimate_partial_f64 return (torch CPU tensors)."""
+    formats qce_estimate_partial_shifted / qce_estimate_partial_f64 / qce_cconst_max return (torch CPU tensors)."""
+    device_type = "cpu"
 
-    def __init__(self, fx, tag, lo, hi):
+    def __init__(self, fx, tag, lo, hi, chol_fail=False):
         from oracle import qce_oracle as O
         y, snr, N, A, n_bits, qtype, quantizer = case_args(fx, tag)
         h, t = O.estimate(fx["means_cplx"], fx["covs_cplx"], fx["weights"], y, snr, N, A, "all", n_bits, qtype,
                           quantizer, return_tables=True)
-        self.lp = O.weighted_log_prob(y, t["means_y"], t["P"], fx["weights"])[:, lo:hi]
+        self.lp_all = O.weighted_log_prob(y, t["means_y"], t["P"], fx["weights"])
+        self.lp = self.lp_all[:, lo:hi]
         self.hk = (np.einsum("knm,bm->bkn", t["W"], y) + t["b"][None])[:, lo:hi]
         c = 2 * np.real(O.log_det_cholesky(t["P"])) + np.log(fx["weights"]) - A.shape[0] * np.log(np.pi)
         self.c = c[lo:hi]
         self.N, self.y, self.h = N, y, h
+        self.chol_fail = chol_fail
+        self._row = {self.y[i].tobytes(): i for i in range(self.y.shape[0])}
 
     def cconst(self):
         return self.c
 
+    def prepare(self, *a, **kw):
+        pass
+
+    def cconst_max(self, out=None, stream=None):
+        # the kernel writes +inf when a Cholesky factorisation of this shard failed (k_cconst_max)
+        out.fill_(float("inf") if self.chol_fail else float(np.max(self.c)))
+        return out
+
     def _rows(self, y):
         import torch
-        # y is a slice of the fixture batch: find its row offset by identity of the data
         yn = y.numpy() if isinstance(y, torch.Tensor) else y
-        for off in range(self.y.shape[0] - yn.shape[0] + 1):
-            if np.array_equal(self.y[off:off + yn.shape[0]], yn):
-                return slice(off, off + yn.shape[0])
-        raise AssertionError("unknown rows")
+        return np.array([self._row[r.tobytes()] for r in yn], dtype=np.int64)
 
     def partial64(self, y, stream=None):
         import torch
@@ -134,12 +142,27 @@ class _OracleShard:
         return torch.from_numpy(m), torch.from_numpy(e.sum(axis=1)), torch.from_numpy(a)
 
     def partial_shifted(self, y, shift, out=None, stream=None):
-        m, s, a = (t.numpy() for t in self.partial64(y))
-        sc = np.exp(m - shift)
-        buf = np.concatenate([(s * sc)[:, None], np.zeros((m.shape[0], 1)), a * sc[:, None]], axis=1)
         import torch
+        m, s, a = (t.numpy() for t in self.partial64(y))
+        sh = float(shift[0]) if isinstance(shift, torch.Tensor) else float(shift)  # (mock only: no kernel here)
+        with np.errstate(under="ignore", over="ignore"):
+            sc = np.exp(m - sh)
+        buf = np.concatenate([(s * sc)[:, None], np.zeros((m.shape[0], 1)), a * sc[:, None]], axis=1)
         out.copy_(torch.from_numpy(buf))
         return out
+
+
+def _make_est(rank, world, fx, tag, chol_fail=False):
+    from quantized_channel_estimation_amd.sharding import ComponentShardEstimator, component_slices
+    K = int(fx["K"])
+    lo, hi = component_slices(K, world)[rank]
+    est = ComponentShardEstimator.__new__(ComponentShardEstimator)
+    est.rank, est.world, est.lo, est.hi, est.group, est._bufs = rank, world, lo, hi, None, {}
+    est._pending = est._flag_acc = None
+    est.shift = None
+    est.dev = _OracleShard(fx, tag, lo, hi, chol_fail=chol_fail)
+    est.N = est.dev.N
+    return est
 
 
 def _pipe_worker(rank, world, port, tag, shift, chunks, scatter, q):
@@ -149,18 +172,16 @@ def _pipe_worker(rank, world, port, tag, shift, chunks, scatter, q):
     os.environ["MASTER_PORT"] = str(port)
     import sys
     sys.path.insert(0, ROOT)
-    from quantized_channel_estimation_amd.sharding import ComponentShardEstimator, component_slices
     dist.init_process_group("gloo", rank=rank, world_size=world)
     fx = load_model("fullmean")
-    K = int(fx["K"])
-    lo, hi = component_slices(K, world)[rank]
-    est = ComponentShardEstimator.__new__(ComponentShardEstimator)
-    est.rank, est.world, est.lo, est.hi, est.group, est._bufs = rank, world, lo, hi, None, {}
-    est.dev = _OracleShard(fx, tag, lo, hi)
-    est.N = est.dev.N
-    t = torch.tensor([float(np.max(est.dev.cconst()))], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    est.shift = float(t.item()) + shift
+    est = _make_est(rank, world, fx, tag)
+    est.prepare(None, 0.0, 1)  # shift = MAX over ranks of max c_k, on the "device" (a CPU tensor here)
+    if shift == "half":
+        # raise the shift so the rows with the smaller max lp leave the normal range (a subset is flagged)
+        mb = est.dev.lp_all.max(axis=1)
+        est.shift += float(np.median(mb) - est.shift.item()) + 667.7
+    else:
+        est.shift += shift
     y = torch.from_numpy(est.dev.y)
     rows, h = est.estimate(y, chunks=chunks, scatter=scatter)
     ref = est.dev.h if rows is None else est.dev.h[rows.numpy()]
@@ -175,23 +196,128 @@ def _pipe_worker(rank, world, port, tag, shift, chunks, scatter, q):
 
 @pytest.mark.parametrize("world,tag,shift,chunks,scatter", [
     (2, "b1_5", 0.0, 3, True), (3, "u2_m10", 0.0, 4, True), (2, "l3_20", 0.0, 1, False),
-    (2, "b1_5", 900.0, 2, True), (3, "b1_5", 900.0, 2, False)])
+    (2, "b1_5", 900.0, 2, True), (3, "b1_5", 900.0, 2, False), (2, "b1_5", "half", 3, True),
+    (3, "u2_m10", "half", None, True), (2, "l3_20", "half", 2, False)])
 def test_pipelined_component_shard_gloo(world, tag, shift, chunks, scatter):
     """The pipelined K-shard estimator over gloo: chunked shifted partials, one SUM collective per chunk
-    (reduce-scatter or all-reduce), FP64 throughout; shift + 900 forces the underflow fallback."""
+    (reduce-scatter or all-reduce), FP64 throughout; shift + 900 flags every row, "half" about half of them
+    (each rank flags only rows it owns under reduce-scatter): only the flagged rows are recombined exactly."""
+    _run(_pipe_worker, world, (tag, shift, chunks, scatter))
+
+
+def _run(target, world, args, check=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, tag, shift, chunks, scatter, q))
-             for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port) + tuple(args) + (q,)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=180) for _ in procs]
     for p in procs:
         p.join(timeout=60)
+    if check is not None:
+        return check(res)
+    scatter = args[-1]
     for rank, err, total, B in res:
         assert err < 1e-12, (rank, err)
         assert total == (B if scatter else B * world)
+
+
+def _nosync_worker(rank, world, port, steps, q):
+    """sync=False steps make no host read of a device value; finish() makes one (the flag word)."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+    sys.path.insert(0, ROOT)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    fx = load_model("fullmean")
+    est = _make_est(rank, world, fx, "b1_5")
+    y = torch.from_numpy(est.dev.y)
+    est.prepare(None, 0.0, 1)
+    counts = {"n": 0}
+    names = ("item", "tolist", "cpu", "numpy", "__float__", "__int__", "__bool__", "__index__")
+    saved = {n: getattr(torch.Tensor, n) for n in names}
+
+    def counting(fn):
+        def f(*a, **kw):
+            counts["n"] += 1
+            return fn(*a, **kw)
+        return f
+    part = est.dev.partial_shifted
+    orig_partial = est.dev.partial_shifted
+
+    def quiet_partial(yy, shift, out=None, stream=None):  # the mock's own host reads are not the estimator's
+        for n in names:
+            setattr(torch.Tensor, n, saved[n])
+        try:
+            return orig_partial(yy, shift, out=out, stream=stream)
+        finally:
+            for n in names:
+                setattr(torch.Tensor, n, counting(saved[n]))
+    est.dev.partial_shifted = quiet_partial
+    for n in names:
+        setattr(torch.Tensor, n, counting(saved[n]))
+    try:
+        for _ in range(steps):
+            est.estimate(y, chunks=2, scatter=True, sync=False)
+        per_steps = counts["n"]
+        counts["n"] = 0
+        rows, h = est.finish()
+        at_finish = counts["n"]
+    finally:
+        for n in names:
+            setattr(torch.Tensor, n, saved[n])
+    est.dev.partial_shifted = part
+    err = rel_fro(h.numpy(), est.dev.h[rows.numpy()])
+    dist.destroy_process_group()
+    q.put((rank, per_steps, at_finish, err))
+
+
+def test_kshard_no_host_sync_per_step_gloo():
+    def check(res):
+        for rank, per_steps, at_finish, err in res:
+            assert per_steps == 0, (rank, per_steps)
+            assert at_finish <= 2, (rank, at_finish)  # flags of the last step + of the whole run
+            assert err < 1e-12
+    _run(_nosync_worker, 2, (3,), check)
+
+
+def _chol_worker(rank, world, port, sync, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+    sys.path.insert(0, ROOT)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    fx = load_model("fullmean")
+    est = _make_est(rank, world, fx, "b1_5", chol_fail=(rank == world - 1))
+    est.prepare(None, 0.0, 1)
+    y = torch.from_numpy(est.dev.y)
+    msg = None
+    try:
+        est.estimate(y, chunks=2, scatter=True, sync=sync)
+        if not sync:
+            est.finish()
+    except ValueError as e:
+        msg = str(e)
+    dist.destroy_process_group()
+    q.put((rank, msg))
+
+
+@pytest.mark.parametrize("sync", [True, False])
+def test_kshard_cholesky_failure_raises_on_every_rank_gloo(sync):
+    """A non-PD Cr_k on one rank (its shard shift is +inf) reaches every rank through the shift's MAX and the
+    step's flag word: each raises the reference's ValueError text (gmm_cplx_bussgang.py:43-46; quirks.npz)."""
+    q = np.load(os.path.join(ROOT, "tests", "golden", "quirks.npz"))
+    want = str(q["nonpd_b1__result"])
+
+    def check(res):
+        for rank, msg in res:
+            assert msg == want, (rank, msg)
+    _run(_chol_worker, 3, (sync,), check)
 
 
 def test_chunk_bounds_cover():
