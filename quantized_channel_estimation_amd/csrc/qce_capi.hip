@@ -1090,11 +1090,12 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
         return fail(QCE_EARG, "unknown mode");
       }
       HIPCHK(m->lp_scr.ensure((size_t)B * m->K));
-      HIPCHK(m->w_scr.ensure((size_t)B * m->K));
+      HIPCHK(m->w64_scr.ensure((size_t)B * m->K));
       fa.lp = m->lp_scr.p;
       HIPCHK(qce_launch_fft_est(fa, 1, st));
-      HIPCHK(qce_launch_select(B, m->K, m->lp_scr.p, kmode, n, p, nullptr, nullptr, m->w_scr.p, st));
-      fa.wts = m->w_scr.p;
+      // FP64 selection weights: the reference sorts complex128-derived proba (gmm_cplx_bussgang.py:213, :235-236)
+      HIPCHK(qce_launch_select(B, m->K, m->lp_scr.p, kmode, n, p, nullptr, nullptr, nullptr, st, m->w64_scr.p));
+      fa.wts = m->w64_scr.p;
       HIPCHK(qce_launch_fft_est(fa, 2, st));
     }
   } else if (mode == QCE_MODE_ALL) {
@@ -1254,7 +1255,14 @@ int qce_estimate_partial_f64(qce_model* m, const double* y, int64_t B, double* m
   }
   if (!m->fft_active && m->f64_active) {
     if ((rc = run_f64(m, dy, B, nullptr, dm, ds, da, st))) return rc;
-  } else {  // Fourier / fast paths keep an f32 accumulator: widen it
+  } else if (m->fft_active) {  // Fourier path: the same kernels with an FP64 accumulator
+    QceFftEstArgs fa = fft_args(m, dy, B);
+    fa.om = dm;
+    fa.os = ds;
+    fa.oa = reinterpret_cast<float*>(da);
+    if (m->fft_mfma) HIPCHK(qce_launch_fft_mfma(fa, 4, st));
+    else HIPCHK(qce_launch_fft_est(fa, 4, st));
+  } else {  // the fast (fp16-split) path keeps an f32 accumulator: widen it
     HIPCHK(m->acc_scr.ensure((size_t)B * 2 * m->N));
     if ((rc = qce_estimate_partial(m, reinterpret_cast<const double*>(dy), B, dm, ds, m->acc_scr.p, QCE_IO_DEVICE,
                                    st)))

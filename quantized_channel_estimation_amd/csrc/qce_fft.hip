@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void k_fft_est(long long B, int N, int n1, int
                                                  const double2* __restrict__ y, const double* __restrict__ rinvT,
                                                  const double2* __restrict__ uT, const double* __restrict__ cprime,
                                                  const double* __restrict__ wT, const double2* __restrict__ bT,
-                                                 const float* __restrict__ wts, double2* __restrict__ h,
+                                                 const double* __restrict__ wts, double2* __restrict__ h,
                                                  double* __restrict__ lp_out, double* __restrict__ om,
                                                  double* __restrict__ os, float* __restrict__ oa) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(256) void k_fft_est(long long B, int N, int n1, int
   } else {
     for (int e = tid; e < TS * K; e += 256) {
       const int r = e / K, k = e % K;
-      P[r * KP + k] = (r < rows) ? (double)wts[(b0 + r) * K + k] : 0.0;
+      P[r * KP + k] = (r < rows) ? wts[(b0 + r) * K + k] : 0.0;
     }
   }
   __syncthreads();
@@ -393,6 +393,11 @@ __global__ __launch_bounds__(256) void k_fft_est(long long B, int N, int n1, int
       at[2 * e] = (float)v.x;
       at[2 * e + 1] = (float)v.y;
     }
+    return;
+  }
+  if (OUT == 4) {  // FP64 accumulator (qce_estimate_partial_f64)
+    double2* at = reinterpret_cast<double2*>(oa) + b0 * N;
+    for (int e = tid; e < rows * N; e += 256) at[e] = T[(e / N) * RS + e % N];
     return;
   }
   double2* ht = h + b0 * N;
@@ -465,6 +470,7 @@ hipError_t qce_launch_fft_est(const QceFftEstArgs& a, int out, hipStream_t st) {
     case 1: return launch_fft_out<1>(a, st);
     case 2: return launch_fft_out<2>(a, st);
     case 3: return launch_fft_out<3>(a, st);
+    case 4: return launch_fft_out<4>(a, st);
     default: return hipErrorInvalidValue;
   }
 }

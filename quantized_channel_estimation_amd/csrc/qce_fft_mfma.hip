@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
       else
         Trow[bin] = make_double2(v.x * f, v.y * f);
     }
-  if (OUT == 3 && kw == 0 && hq == 0 && srow < rows) {
+  if ((OUT == 3 || OUT == 4) && kw == 0 && hq == 0 && srow < rows) {
     om[b0 + srow] = m;
     os[b0 + srow] = ssum;
   }
@@ -333,6 +333,12 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
       const double2 v = T[(e >> lgN) * RS + (e & (N - 1))];
       at[e] = make_float2((float)v.x, (float)v.y);
     }
+    return;
+  }
+  if (OUT == 4) {  // FP64 accumulator of the K-shard partial (qce_estimate_partial_f64)
+    double2* at = reinterpret_cast<double2*>(oa) + b0 * N;
+#pragma unroll 4
+    for (int e = tid; e < rows * N; e += 256) at[e] = T[(e >> lgN) * RS + (e & (N - 1))];
     return;
   }
   double2* ht = h + b0 * N;
@@ -667,7 +673,7 @@ __global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wave(long long B, long 
           else
             Trow[bin] = make_double2(q.x * f, q.y * f);
         }
-      if (OUT == 3 && hq == 0 && col < rows) {
+      if ((OUT == 3 || OUT == 4) && hq == 0 && col < rows) {
         om[b0 + col] = m;
         os[b0 + col] = ssum;
       }
@@ -689,6 +695,13 @@ __global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wave(long long B, long 
             const double2 q = T[r * RS + (e & (N - 1))];
             at[e] = make_float2((float)q.x, (float)q.y);
           }
+        }
+      } else if (OUT == 4) {
+        double2* at = reinterpret_cast<double2*>(oa) + b0 * N;
+#pragma unroll
+        for (int i = 0; i < N / 4; ++i) {
+          const int e = lane + 64 * i, r = e >> lgN;
+          if (r < rows) at[e] = T[r * RS + (e & (N - 1))];
         }
       } else {
         double2* ht = h + b0 * N;
@@ -872,6 +885,7 @@ hipError_t qce_launch_fft_mfma(const QceFftEstArgs& a, int out, hipStream_t st) 
   if (a.B <= 0) return hipSuccess;
   if (out == 0) return a.has_mean ? launch_mfma_out<0, true>(a, st) : launch_mfma_out<0, false>(a, st);
   if (out == 3) return a.has_mean ? launch_mfma_out<3, true>(a, st) : launch_mfma_out<3, false>(a, st);
+  if (out == 4) return a.has_mean ? launch_mfma_out<4, true>(a, st) : launch_mfma_out<4, false>(a, st);
   return hipErrorInvalidValue;
 }
 

@@ -168,11 +168,11 @@ struct QceFftEstArgs {
   const double* cprime;
   const double* wT;
   const double2* bT;
-  const float* wts;  // selection weights (out = 2)
+  const double* wts;  // FP64 selection weights (out = 2; k_select's wts64)
   double2* h;
   double* lp;        // out = 1
-  double *om, *os;   // out = 3
-  float* oa;
+  double *om, *os;   // out = 3, 4
+  float* oa;         // out = 3: f32 (B, 2N); out = 4: the same buffer holds an f64 (B, 2N) accumulator
   // MFMA kernel tables (qce_fft_mfma.hip, storage order, components padded to Kp)
   int Kp;
   const double *pr, *pur, *pui, *pc, *pw, *pbr, *pbi;
@@ -183,9 +183,9 @@ int qce_fft_tile(int N, int K);  // 0: no tile fits (K too large)
 hipError_t qce_launch_fft_struct(int K, int N, int n1, int n2, double tol, const double2* covs, const double2* means,
                                  double* ceig, double2* col0, double2* mspec, int* bad, hipStream_t st);
 hipError_t qce_launch_fft_prep(const QceFftPrepArgs& a, hipStream_t st);
-// out: 0 'all' h, 1 lp, 2 weighted h, 3 K-shard partial
+// out: 0 'all' h, 1 lp, 2 weighted h, 3 K-shard partial (f32 acc), 4 K-shard partial (f64 acc)
 hipError_t qce_launch_fft_est(const QceFftEstArgs& a, int out, hipStream_t st);
-// MFMA Fourier kernel (qce_fft_mfma.hip): N in {16, ..., 256}; out 0 'all' h, 3 K-shard partial
+// MFMA Fourier kernel (qce_fft_mfma.hip): N in {16, ..., 256}; out 0 'all' h, 3 / 4 K-shard partial (f32 / f64)
 bool qce_fft_mfma_shape(int N);
 int qce_fft_kpad(int K);
 hipError_t qce_launch_fft_pack(const QceFftEstArgs& a, const double* rinvT, const double2* uT, const double* cprime,

@@ -70,15 +70,15 @@ def test_cfg5_fourier_and_dense(fft, monkeypatch):
         hg = g.estimate_from_y(y, 5.0, N, None, mode, 2, "uniform", qz)
         assert g._dev.structure()[2] == (1 if fft == "1" else 0)
         ho = O.estimate(means, covs, w, y, 5.0, N, None, mode, 2, "uniform", qz)
-        # Fourier path: FP64 throughout ('all'); selective modes carry its fp32 selection weights.  Dense
-        # N = 256: 'all' runs the fp16-split kernel (no FP64 fused instance at 256), selective modes FP64.
+        # Fourier path: FP64 throughout, selection weights included.  Dense N = 256: 'all' runs the
+        # fp16-split kernel (no FP64 fused instance at 256), selective modes FP64.
         if fft == "1":
-            tol = 1e-9 if mode == "all" else 1e-6
+            tol = F64_TOL
         else:
             tol = H_TOL if mode == "all" else F64_TOL
         assert rel_fro(hg, ho) < tol, (fft, mode, rel_fro(hg, ho))
     h_all = O.estimate(means, covs, w, y, 5.0, N, None, "all", 2, "uniform", qz)
-    tol = 1e-6 if fft == "1" else H_TOL  # the Fourier / fp16-split partials carry an f32 accumulator
+    tol = F64_TOL if fft == "1" else H_TOL  # shifted partials: FP64 (Fourier); the fp16-split partial at 256
     assert rel_fro(_shard_combine(means, covs, w, y, 2, [(0, 64), (64, 128)]), h_all) < tol
 
 

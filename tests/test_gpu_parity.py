@@ -364,9 +364,9 @@ def test_fourier_path_vs_oracle_and_dense(K, N, blocks, B, n_bits, qtype, mean, 
         hg = g.estimate_from_y(y, 5.0, N, None, mode, n_bits, qtype, qz)
         assert g._dev.structure()[2] == 1
         ho = O.estimate(means, covs, w, y, 5.0, N, None, mode, n_bits, qtype, qz)
-        # FP64 end to end; the selective modes carry fp32 selection weights (k_select); 1 bit: the
-        # arcsine-law sensitivity of the dense restatement (see test_logprob_proba_labels_after_estimate)
-        tol = (1e-9 if n_bits != 1 else 1e-7) if mode in ("all", 1) else 1e-6
+        # FP64 end to end, the selection weights included (k_select's FP64 weights); 1 bit: the arcsine-law
+        # sensitivity of the dense restatement (see test_logprob_proba_labels_after_estimate)
+        tol = 1e-9 if n_bits != 1 else 1e-7
         assert rel_fro(hg, ho) < tol, (mode, rel_fro(hg, ho))
         res[mode] = hg
     t = O.prepare(means, covs, np.eye(N), 5.0, n_bits, qtype, qz)
@@ -432,13 +432,16 @@ def test_fourier_mfma_kernel_vs_lds_kernel(K, N, blocks, B, n_bits, mean, monkey
         dm = _lib.DeviceModel(means, covs, w)
         dm.prepare(None, 5.0, float(n_bits))
         assert dm.structure()[2] == 1
-        out[kern] = (dm.estimate(y), combine_partials_numpy([dm.partial(y)], N))
+        out[kern] = (dm.estimate(y), combine_partials_numpy([dm.partial(y)], N),
+                     combine_partials_numpy([dm.partial64(y)], N))
         dm.close()
     ho = O.estimate(means, covs, w, y, 5.0, N, None, "all", n_bits, qtype, qz)
     tol = 1e-9 if n_bits != 1 else 1e-7
     assert rel_fro(out["mfma"][0], ho) < tol
     assert rel_fro(out["mfma"][0], out["lds"][0]) < 1e-12
-    assert rel_fro(out["mfma"][1], ho) < 1e-6  # partial acc is fp32
+    assert rel_fro(out["mfma"][1], ho) < 1e-6  # qce_estimate_partial's acc is fp32 by its ABI
+    for kern in ("mfma", "lds"):  # qce_estimate_partial_f64: the FP64 accumulator of the same kernels
+        assert rel_fro(out[kern][2], ho) < tol, kern
 
 
 @pytest.mark.parametrize("K,N,blocks,B,n_bits,qtype,mean", [
