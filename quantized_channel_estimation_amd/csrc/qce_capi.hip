@@ -100,6 +100,9 @@ struct qce_model {
   // FP64 fused-kernel tables (qce_estimate_f64.hip) and its cut-tile scratch
   DevBuf<char> pack_f64;
   int f64_active = 0;  // the last dense prepare packed FP64 tables: 'all' / partial run k_est_all_f64
+  DevBuf<char> pack_ws;
+  int f64_wide = 0;    // ... or, beyond padded 128, the two-pass FP64 path (qce_wsum_f64.hip)
+  int pack64_valid = 0;  // pack64 (the k_lp_f64 table) built without pack32
   DevBuf<double> fp_m, fp_s, fp_a;
   DevBuf<double> part_a64;  // FP64 partial accumulator behind the f32 qce_estimate_partial
   DevBuf<double> fp_pack;   // host-I/O staging of qce_estimate_partial_shifted
@@ -180,8 +183,21 @@ int stage_input(qce_model* m, const double* y, long long B, int io, hipStream_t 
 
 int ensure_packs(qce_model* m, hipStream_t st) {
   if (m->packs_valid) return QCE_OK;
-  HIPCHK(qce_launch_pack_selective(m->pack_args, st));
+  QcePrepareArgs p = m->pack_args;
+  if (m->pack64_valid) p.pack64 = nullptr;
+  HIPCHK(qce_launch_pack_selective(p, st));
   m->packs_valid = 1;
+  m->pack64_valid = 1;
+  return QCE_OK;
+}
+
+// the FP64 log-prob table alone (k_lp_f64), for the two-pass FP64 'all' path
+int ensure_pack64(qce_model* m, hipStream_t st) {
+  if (m->packs_valid || m->pack64_valid) return QCE_OK;
+  QcePrepareArgs p = m->pack_args;
+  p.pack32 = nullptr;
+  HIPCHK(qce_launch_pack_selective(p, st));
+  m->pack64_valid = 1;
   return QCE_OK;
 }
 
@@ -264,6 +280,45 @@ int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om
   g_f64_stamp_records = nwg * a.waves;
 #endif
   HIPCHK(qce_launch_est_f64(a, h == nullptr, st));
+  return QCE_OK;
+}
+
+// 'all' mode / K-shard partials in FP64 beyond padded 128 (qce_wsum_f64.hip): lp on FP64 MFMA, the weights of
+// the requested output (wmode 0: proba -> h; 1: (m, s, acc); 2: shifted packed rows), the weighted filter sum
+int run_wide(qce_model* m, const double2* dy, long long B, int wmode, double2* h, double* om, double* os, double* oa,
+             double* pk, const double* shift, hipStream_t st) {
+  const size_t BK = (size_t)B * m->K;
+  HIPCHK(m->lp_scr.ensure(BK));
+  HIPCHK(m->w64_scr.ensure(BK));
+  if (int rc = ensure_pack64(m, st)) return rc;
+  QceEstArgs a = est_args(m, dy, B);
+  HIPCHK(qce_launch_lp(a, m->lp_scr.p, st));
+  HIPCHK(qce_launch_wsum_weights(B, m->K, m->lp_scr.p, wmode, shift, m->w64_scr.p, om, os, pk, 2LL * m->N + 2, st));
+  QceWsumArgs w;
+  w.B = B;
+  w.M = m->M;
+  w.N = m->N;
+  w.K = m->K;
+  w.MP = m->MP;
+  w.NP = m->NP;
+  w.has_mean = m->has_mean;
+  w.y = dy;
+  w.pack = m->pack_ws.p;
+  w.wT = m->w64_scr.p;
+  if (wmode == 0) {
+    w.out = h;
+    w.ostride = m->N;
+    w.ooff = 0;
+  } else if (wmode == 1) {
+    w.out = reinterpret_cast<double2*>(oa);
+    w.ostride = m->N;
+    w.ooff = 0;
+  } else {
+    w.out = reinterpret_cast<double2*>(pk);
+    w.ostride = m->N + 1;
+    w.ooff = 1;
+  }
+  HIPCHK(qce_launch_wsum(w, st));
   return QCE_OK;
 }
 
@@ -626,6 +681,7 @@ int qce_model_destroy(qce_model* m) {
   m->sp_a.release();
   m->yflag.release();
   m->pack_f64.release();
+  m->pack_ws.release();
   for (auto* b : {&m->fp_m, &m->fp_s, &m->fp_a, &m->part_a64, &m->fp_pack, &m->w64_scr, &m->shift_scr})
     b->release();
   m->WT.release();
@@ -888,12 +944,19 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
   p.stride64 = s64;
   m->pack_args = p;
   m->packs_valid = 0;
+  m->pack64_valid = 0;
   m->wt_valid = 0;
   p.pack32 = nullptr;  // selective-mode / log-prob tables are packed on first use (ensure_packs)
   p.pack64 = nullptr;
   HIPCHK(qce_launch_prepare(p, st));
   m->f64_active = want_f64(m) && qce_f64_shape(MP, NP);
-  if (m->f64_active) {
+  m->f64_wide = want_f64(m) && !m->f64_active && qce_wsum_shape(MP, NP);
+  if (m->f64_wide) {
+    // FP64 filter tables of the two-pass path; the log-prob table is packed on first use (ensure_pack64)
+    HIPCHK(m->pack_ws.ensure((size_t)qce_pack_wsum_bytes(MP, NP, m->has_mean) * K));
+    HIPCHK(qce_launch_pack_wsum(K, M, N, MP, NP, m->has_mean, m->W.p, m->bvec.p,
+                                reinterpret_cast<double*>(m->pack_ws.p), st));
+  } else if (m->f64_active) {
     // FP64 tables of the fused kernel (reference precision)
     HIPCHK(m->pack_f64.ensure((size_t)qce_pack_f64all_bytes(MP, NP, m->has_mean) * K));
     HIPCHK(qce_launch_pack_f64all(K, M, N, MP, NP, m->has_mean, m->Linv.p, m->W.p, m->q0.p, m->bvec.p,
@@ -1101,6 +1164,8 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
   } else if (mode == QCE_MODE_ALL) {
     if (m->f64_active) {
       if ((rc = run_f64(m, dy, B, dh, nullptr, nullptr, nullptr, st))) return rc;
+    } else if (m->f64_wide) {
+      if ((rc = run_wide(m, dy, B, 0, dh, nullptr, nullptr, nullptr, nullptr, nullptr, st))) return rc;
     } else if (use_h2() || !qce_shape_supported(m->MP, m->NP)) {
       if ((rc = run_h2(m, dy, B, dh, nullptr, nullptr, nullptr, st))) return rc;
     } else {
@@ -1214,9 +1279,13 @@ int qce_estimate_partial(qce_model* m, const double* y, int64_t B, double* m_out
     fa.oa = da;
     if (m->fft_mfma) HIPCHK(qce_launch_fft_mfma(fa, 3, st));
     else HIPCHK(qce_launch_fft_est(fa, 3, st));
-  } else if (m->f64_active) {  // FP64 partial, rounded to the f32 accumulator of this entry point
+  } else if (m->f64_active || m->f64_wide) {  // FP64 partial, rounded to the f32 accumulator of this entry point
     HIPCHK(m->part_a64.ensure((size_t)B * 2 * m->N));
-    if ((rc = run_f64(m, dy, B, nullptr, dm, ds, m->part_a64.p, st))) return rc;
+    if (m->f64_active) {
+      if ((rc = run_f64(m, dy, B, nullptr, dm, ds, m->part_a64.p, st))) return rc;
+    } else if ((rc = run_wide(m, dy, B, 1, nullptr, dm, ds, m->part_a64.p, nullptr, nullptr, st))) {
+      return rc;
+    }
     HIPCHK(qce_launch_f64_to_f32(m->part_a64.p, da, (long long)B * 2 * m->N, st));
   } else if (use_h2() || !qce_shape_supported(m->MP, m->NP)) {
     if ((rc = run_h2(m, dy, B, nullptr, dm, ds, da, st))) return rc;
@@ -1255,6 +1324,8 @@ int qce_estimate_partial_f64(qce_model* m, const double* y, int64_t B, double* m
   }
   if (!m->fft_active && m->f64_active) {
     if ((rc = run_f64(m, dy, B, nullptr, dm, ds, da, st))) return rc;
+  } else if (!m->fft_active && m->f64_wide) {
+    if ((rc = run_wide(m, dy, B, 1, nullptr, dm, ds, da, nullptr, nullptr, st))) return rc;
   } else if (m->fft_active) {  // Fourier path: the same kernels with an FP64 accumulator
     QceFftEstArgs fa = fft_args(m, dy, B);
     fa.om = dm;
@@ -1300,6 +1371,8 @@ int qce_estimate_partial_shifted(qce_model* m, const double* y, int64_t B, const
   }
   if (!m->fft_active && m->f64_active) {
     if ((rc = run_f64(m, dy, B, nullptr, nullptr, nullptr, nullptr, st, dp, dshift))) return rc;
+  } else if (!m->fft_active && m->f64_wide) {
+    if ((rc = run_wide(m, dy, B, 2, nullptr, nullptr, nullptr, nullptr, dp, dshift, st))) return rc;
   } else {  // other paths: their (m, s, acc) partial, scaled and packed
     HIPCHK(m->m_scr.ensure((size_t)B));
     HIPCHK(m->s_scr.ensure((size_t)B));

@@ -115,6 +115,26 @@ hipError_t qce_launch_pack_shifted(long long B, int N, const double* m, const do
 // out[0] = max_k cconst[k] (device), the local part of the K-shard shift M*
 hipError_t qce_launch_cconst_max(int K, const double* cconst, const int* status, double* out, hipStream_t st);
 hipError_t qce_launch_f64_to_f32(const double* a, float* b, long long n, hipStream_t st);
+// FP64 'all' mode beyond the fused kernel's 128 (qce_wsum_f64.hip): lp (k_lp_f64) -> weights -> weighted filter sum
+struct QceWsumArgs {
+  long long B;
+  int M, N, K, MP, NP, has_mean;
+  const double2* y;
+  const char* pack;   // K x qce_pack_wsum_bytes
+  const double* wT;   // K x B weights
+  double2* out;       // out[b * ostride + ooff + i]
+  long long ostride;  // double2 elements per output row
+  int ooff;
+};
+bool qce_wsum_shape(int MP, int NP);
+long long qce_pack_wsum_bytes(int MP, int NP, int has_mean);  // per component
+hipError_t qce_launch_pack_wsum(int K, int M, int N, int MP, int NP, int has_mean, const double2* W,
+                                const double2* bvec, double* pack, hipStream_t st);
+// mode 0: proba (K x B), 1: e^{lp - m} with (m, s) -> om / os, 2: e^{lp - shift} with s -> pk[b * pk_stride]
+hipError_t qce_launch_wsum_weights(long long B, int K, const double* lp, int mode, const double* shift, double* wT,
+                                   double* om, double* os, double* pk, long long pk_stride, hipStream_t st);
+hipError_t qce_launch_wsum(const QceWsumArgs& a, hipStream_t st);
+
 hipError_t qce_launch_f32_to_f64(const float* a, double* b, long long n, hipStream_t st);
 
 // *flag |= (some y * y_scale is not exactly representable in fp16); n = doubles in y

@@ -70,16 +70,56 @@ def test_cfg5_fourier_and_dense(fft, monkeypatch):
         hg = g.estimate_from_y(y, 5.0, N, None, mode, 2, "uniform", qz)
         assert g._dev.structure()[2] == (1 if fft == "1" else 0)
         ho = O.estimate(means, covs, w, y, 5.0, N, None, mode, 2, "uniform", qz)
-        # Fourier path: FP64 throughout, selection weights included.  Dense N = 256: 'all' runs the
-        # fp16-split kernel (no FP64 fused instance at 256), selective modes FP64.
-        if fft == "1":
-            tol = F64_TOL
-        else:
-            tol = H_TOL if mode == "all" else F64_TOL
-        assert rel_fro(hg, ho) < tol, (fft, mode, rel_fro(hg, ho))
+        # FP64 throughout on both paths: Fourier (selection weights included) and dense N = 256 ('all' on the
+        # two-pass FP64 kernels k_lp_f64 + k_wsum_f64)
+        assert rel_fro(hg, ho) < F64_TOL, (fft, mode, rel_fro(hg, ho))
     h_all = O.estimate(means, covs, w, y, 5.0, N, None, "all", 2, "uniform", qz)
-    tol = F64_TOL if fft == "1" else H_TOL  # shifted partials: FP64 (Fourier); the fp16-split partial at 256
-    assert rel_fro(_shard_combine(means, covs, w, y, 2, [(0, 64), (64, 128)]), h_all) < tol
+    assert rel_fro(_shard_combine(means, covs, w, y, 2, [(0, 64), (64, 128)]), h_all) < F64_TOL
+
+
+@pytest.mark.parametrize("n_pilots,N,K,n_bits,mean", [(4, 64, 32, 1, False), (4, 64, 24, 3, True),
+                                                     (2, 128, 16, 1, False), (1, 256, 12, np.inf, True),
+                                                     (8, 32, 20, 2, False)])
+def test_dense_padded_256_fp64(n_pilots, N, K, n_bits, mean):
+    """Dense shapes whose padded observation or channel dimension is 256 (M = n_pilots N with the scripts'
+    pilot matrix, utils.py:337-367; or N = 256): every mode and the K-shard partials in FP64 at 1e-9."""
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import Gmm_nbit, inputs, _lib
+    from quantized_channel_estimation_amd.sharding import combine_packed_numpy, combine_partials_numpy
+    rng = np.random.default_rng(600 + N + K)
+    means, covs, w = inputs.synthetic_model(K, N, seed=7 + K)
+    if mean:
+        means = 0.3 * (rng.standard_normal((K, N)) + 1j * rng.standard_normal((K, N)))
+    A = inputs.get_pilot_matrix(N, n_pilots, n_bits)
+    B = 300
+    h, _ = inputs.scm_generate(B, 1, N, rng, n_path=3)
+    h = h[:, 0, :].astype(complex)
+    qtype = "uniform"
+    qz = (None, None, None)
+    if n_bits not in (1, np.inf):
+        qz = inputs.get_quantizer([5.0], n_bits, qtype)[5.0]
+    y = inputs.get_observation_nbit(h, 5.0, A, n_bits, qz[0], qz[1], rng=rng)
+    g = Gmm_nbit.from_params(means, covs, w)
+    for mode in ("all", 1, 3, 0.9):
+        hg = g.estimate_from_y(y, 5.0, N, A, mode, n_bits, qtype, qz)
+        ho = O.estimate(means, covs, w, y, 5.0, N, A, mode, n_bits, qtype, qz)
+        # 1 bit with a non-identity A: the arcsine-law sensitivity documented in test_gpu_parity (1e-8 there)
+        tol = 1e-7 if (n_bits == 1 and n_pilots > 1) else F64_TOL
+        assert rel_fro(hg, ho) < tol, (mode, rel_fro(hg, ho))
+        if mode == "all":
+            h_all = hg
+    # K-shard partials of the same path: (m, s, acc) in FP64, and the shifted packed rows
+    cuts = [(0, K // 2), (K // 2, K)]
+    models = []
+    for lo, hi in cuts:
+        d = _lib.DeviceModel(means[lo:hi], covs[lo:hi], w[lo:hi])
+        d.prepare(A, 5.0, float(n_bits), _lib.QUANT_UNIFORM)
+        models.append(d)
+    shift = max(d.cconst_max() for d in models)
+    hp = combine_packed_numpy([d.partial_shifted(y, shift) for d in models])
+    assert rel_fro(hp, h_all) < 1e-12
+    hm = combine_partials_numpy([tuple(d.partial64(y)) for d in models], N)
+    assert rel_fro(hm, h_all) < 1e-12
 
 
 @pytest.mark.gpu
