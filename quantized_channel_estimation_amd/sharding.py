@@ -150,6 +150,7 @@ class ComponentShardEstimator:
         self._bufs = {}
         self._pending = None
         self._flag_acc = None
+        self._chol_local = False
 
     def _on_gpu(self):
         return getattr(self.dev, "device_type", "cuda") == "cuda"
@@ -166,10 +167,12 @@ class ComponentShardEstimator:
             s = stream if stream is not None else cur.cuda_stream
         else:
             dev, cur, s = torch.device("cpu"), None, None
+        self._chol_local = False
         self.dev.prepare(A, snr_db, n_bits, quant_kind, thresholds, labels, stream=s)
         if not isinstance(self.shift, torch.Tensor) or self.shift.device != dev:
             self.shift = torch.empty(1, dtype=torch.float64, device=dev)
-        self.dev.cconst_max(out=self.shift, stream=s)
+        if not self._guarded(self.dev.cconst_max, out=self.shift, stream=s):
+            self.shift.fill_(float("inf"))  # the failure rides the shift as the kernel would have written it
         if cur is not None and s != cur.cuda_stream:  # the collective runs behind torch's current stream
             ev = torch.cuda.Event()
             ev.record(torch.cuda.ExternalStream(s, device=dev))
@@ -185,11 +188,28 @@ class ComponentShardEstimator:
             self._bufs[key] = b
         return b
 
+    def _guarded(self, fn, *a, **kw):
+        """Run a device call of this rank; a Cholesky failure the library has already surfaced (it reports the
+        deferred status at the first call that finds it complete) is recorded instead of raised, so every rank
+        still reaches the step's collectives and all of them raise together at finish()."""
+        if getattr(self, "_chol_local", False):
+            return False
+        try:
+            fn(*a, **kw)
+            return True
+        except ValueError as e:
+            if str(e) != _lib.CHOL_MESSAGE:
+                raise
+            self._chol_local = True
+            return False
+
     def _chol_flag(self, device):
         import torch
+        local = 1.0 if getattr(self, "_chol_local", False) else 0.0
         if isinstance(self.shift, torch.Tensor):
-            return torch.isinf(self.shift).to(torch.float64).reshape(1)
-        return torch.tensor([1.0 if math.isinf(float(self.shift)) else 0.0], dtype=torch.float64, device=device)
+            return torch.clamp(torch.isinf(self.shift).to(torch.float64).reshape(1), min=local)
+        return torch.tensor([1.0 if (local or math.isinf(float(self.shift))) else 0.0], dtype=torch.float64,
+                            device=device)
 
     def estimate(self, y, chunks=None, scatter=True, sync=True):
         """'all'-mode estimates of y (B, M) complex128 tensor.
@@ -215,7 +235,8 @@ class ComponentShardEstimator:
             pk = self._buf(("pk", i), (npad, W), dev)
             if npad > n:
                 pk[n:].zero_()
-            self.dev.partial_shifted(y[lo:hi], self.shift, out=pk[:n], stream=stream)
+            if not self._guarded(self.dev.partial_shifted, y[lo:hi], self.shift, out=pk[:n], stream=stream):
+                pk[:n].zero_()
             if use_rs:
                 out = self._buf(("rs", i), (npad // self.world, W), dev)
                 works.append(dist.reduce_scatter_tensor(out, pk, op=dist.ReduceOp.SUM, group=self.group,

@@ -1,6 +1,7 @@
 """K-shard estimator on the GPU, two ranks sharing the one GPU of the box over gloo (the driver's 8-GPU node runs
 the same code over RCCL): a non-PD Cr_k on one rank raises the reference's ValueError on every rank
 (gmm_cplx_bussgang.py:43-46, quirks.npz), and rows flagged for exact recombination are recombined exactly."""
+import datetime
 import os
 import socket
 
@@ -28,9 +29,13 @@ def _run(target, world, args):
     procs = [ctx.Process(target=target, args=(r, world, port) + tuple(args) + (q,)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=240) for _ in procs]
-    for p in procs:
-        p.join(timeout=60)
+    try:
+        res = [q.get(timeout=120) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
     return res
 
 
@@ -43,7 +48,7 @@ def _chol_worker(rank, world, port, sync, q):
     import torch
     import torch.distributed as dist
     from quantized_channel_estimation_amd.sharding import ComponentShardEstimator
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
     qx = np.load(os.path.join(ROOT, "tests", "golden", "quirks.npz"))
     out = []
     for tag, nb in (("nonpd_inf", np.inf), ("nonpd_b1", 1)):
@@ -82,7 +87,7 @@ def _repair_worker(rank, world, port, q):
     from conftest import load_model, case_args
     from oracle import qce_oracle as O
     from quantized_channel_estimation_amd.sharding import ComponentShardEstimator, UNDERFLOW_S
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
     fx = load_model("fullmean")
     y, snr, N, A, n_bits, qtype, quantizer = case_args(fx, "b1_5")
     href, t = O.estimate(fx["means_cplx"], fx["covs_cplx"], fx["weights"], y, snr, N, A, "all", n_bits, qtype,

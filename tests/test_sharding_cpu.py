@@ -3,6 +3,7 @@
 The per-shard partials (running max m, s = sum e^{lp-m}, acc = sum e^{lp-m} h_k) are produced by
 the FP64 oracle here (the GPU produces them with qce_estimate_partial); the distributed combine
 (one SUM all-reduce + the underflow fallback) must reproduce the full 'all'-mode estimate."""
+import datetime
 import os
 import socket
 
@@ -47,7 +48,7 @@ def _worker(rank, world, port, tag, shift, q):
     import sys
     sys.path.insert(0, ROOT)
     from quantized_channel_estimation_amd.sharding import combine_partials_dist, component_slices
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
     fx = load_model("fullmean")
     K, N = int(fx["K"]), int(fx["N"])
     lo, hi = component_slices(K, world)[rank]
@@ -100,7 +101,7 @@ class _OracleShard:
     formats qce_estimate_partial_shifted / qce_estimate_partial_f64 / qce_cconst_max return (torch CPU tensors)."""
     device_type = "cpu"
 
-    def __init__(self, fx, tag, lo, hi, chol_fail=False):
+    def __init__(self, fx, tag, lo, hi, chol_fail=False, raise_at=None):
         from oracle import qce_oracle as O
         y, snr, N, A, n_bits, qtype, quantizer = case_args(fx, tag)
         h, t = O.estimate(fx["means_cplx"], fx["covs_cplx"], fx["weights"], y, snr, N, A, "all", n_bits, qtype,
@@ -112,6 +113,9 @@ class _OracleShard:
         self.c = c[lo:hi]
         self.N, self.y, self.h = N, y, h
         self.chol_fail = chol_fail
+        # where the library surfaces a failed factorisation as ValueError instead (its deferred status read by a
+        # later call): None (only the +inf shift), "cconst" or "partial"
+        self.raise_at = raise_at if chol_fail else None
         self._row = {self.y[i].tobytes(): i for i in range(self.y.shape[0])}
 
     def cconst(self):
@@ -122,6 +126,9 @@ class _OracleShard:
 
     def cconst_max(self, out=None, stream=None):
         # the kernel writes +inf when a Cholesky factorisation of this shard failed (k_cconst_max)
+        if self.raise_at == "cconst":
+            from quantized_channel_estimation_amd import _lib
+            raise ValueError(_lib.CHOL_MESSAGE)
         out.fill_(float("inf") if self.chol_fail else float(np.max(self.c)))
         return out
 
@@ -143,6 +150,9 @@ class _OracleShard:
 
     def partial_shifted(self, y, shift, out=None, stream=None):
         import torch
+        if self.raise_at == "partial":
+            from quantized_channel_estimation_amd import _lib
+            raise ValueError(_lib.CHOL_MESSAGE)
         m, s, a = (t.numpy() for t in self.partial64(y))
         sh = float(shift[0]) if isinstance(shift, torch.Tensor) else float(shift)  # (mock only: no kernel here)
         with np.errstate(under="ignore", over="ignore"):
@@ -152,15 +162,16 @@ class _OracleShard:
         return out
 
 
-def _make_est(rank, world, fx, tag, chol_fail=False):
+def _make_est(rank, world, fx, tag, chol_fail=False, raise_at=None):
     from quantized_channel_estimation_amd.sharding import ComponentShardEstimator, component_slices
     K = int(fx["K"])
     lo, hi = component_slices(K, world)[rank]
     est = ComponentShardEstimator.__new__(ComponentShardEstimator)
     est.rank, est.world, est.lo, est.hi, est.group, est._bufs = rank, world, lo, hi, None, {}
     est._pending = est._flag_acc = None
+    est._chol_local = False
     est.shift = None
-    est.dev = _OracleShard(fx, tag, lo, hi, chol_fail=chol_fail)
+    est.dev = _OracleShard(fx, tag, lo, hi, chol_fail=chol_fail, raise_at=raise_at)
     est.N = est.dev.N
     return est
 
@@ -172,7 +183,7 @@ def _pipe_worker(rank, world, port, tag, shift, chunks, scatter, q):
     os.environ["MASTER_PORT"] = str(port)
     import sys
     sys.path.insert(0, ROOT)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
     fx = load_model("fullmean")
     est = _make_est(rank, world, fx, tag)
     est.prepare(None, 0.0, 1)  # shift = MAX over ranks of max c_k, on the "device" (a CPU tensor here)
@@ -231,7 +242,7 @@ def _nosync_worker(rank, world, port, steps, q):
     os.environ["MASTER_PORT"] = str(port)
     import sys
     sys.path.insert(0, ROOT)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
     fx = load_model("fullmean")
     est = _make_est(rank, world, fx, "b1_5")
     y = torch.from_numpy(est.dev.y)
@@ -284,16 +295,16 @@ def test_kshard_no_host_sync_per_step_gloo():
     _run(_nosync_worker, 2, (3,), check)
 
 
-def _chol_worker(rank, world, port, sync, q):
+def _chol_worker(rank, world, port, sync, raise_at, q):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import sys
     sys.path.insert(0, ROOT)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
     fx = load_model("fullmean")
-    est = _make_est(rank, world, fx, "b1_5", chol_fail=(rank == world - 1))
+    est = _make_est(rank, world, fx, "b1_5", chol_fail=(rank == world - 1), raise_at=raise_at)
     est.prepare(None, 0.0, 1)
     y = torch.from_numpy(est.dev.y)
     msg = None
@@ -307,17 +318,19 @@ def _chol_worker(rank, world, port, sync, q):
     q.put((rank, msg))
 
 
-@pytest.mark.parametrize("sync", [True, False])
-def test_kshard_cholesky_failure_raises_on_every_rank_gloo(sync):
+@pytest.mark.parametrize("sync,raise_at", [(True, None), (False, None), (True, "partial"), (False, "cconst")])
+def test_kshard_cholesky_failure_raises_on_every_rank_gloo(sync, raise_at):
     """A non-PD Cr_k on one rank (its shard shift is +inf) reaches every rank through the shift's MAX and the
-    step's flag word: each raises the reference's ValueError text (gmm_cplx_bussgang.py:43-46; quirks.npz)."""
+    step's flag word: each raises the reference's ValueError text (gmm_cplx_bussgang.py:43-46; quirks.npz).
+    raise_at: the library reported the failure from a later device call on that rank instead -- the rank must
+    still join every collective of the step (no hang) and all ranks raise together."""
     q = np.load(os.path.join(ROOT, "tests", "golden", "quirks.npz"))
     want = str(q["nonpd_b1__result"])
 
     def check(res):
         for rank, msg in res:
             assert msg == want, (rank, msg)
-    _run(_chol_worker, 3, (sync,), check)
+    _run(_chol_worker, 3, (sync, raise_at), check)
 
 
 def test_chunk_bounds_cover():
