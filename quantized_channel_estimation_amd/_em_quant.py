@@ -1,21 +1,25 @@
-"""EM of ``Gmm_quant.fit`` on quantised observations, 'full' covariances (reference gmm_cplx_quant.py:103-189
-fit, :484-602 fit_predict / _initialize_parameters / _initialize, :640-731 _e_step / _m_step,
-:732-854 estimate_gaussian_parameters / estimate_gaussian_covariances_full; cov_est_quant.py:31-88
-est_cov_from_quant; utils.py:651-700 gauss_newt_solve).
+"""EM of ``Gmm_quant.fit`` on quantised observations (reference gmm_cplx_quant.py:103-189 fit, :484-602
+fit_predict / _initialize_parameters / _initialize, :640-731 _e_step / _m_step, :732-854
+estimate_gaussian_parameters / estimate_gaussian_covariances_full, :880-945 estimate_gaussian_covariances_inv;
+cov_est_quant.py:31-88 est_cov_from_quant; utils.py:651-700 gauss_newt_solve).
 
 The model of the observations is a GMM with two covariance sets: ``covariances_`` (the recovered
 unquantised covariances, what the estimator uses) and ``covariances_quant`` (the covariances of the
 quantised data, what the E-step evaluates).  Per iteration the B-sized work runs in libqce.so: the E-step
 on ``covariances_quant`` (``qce_em_estep``), the weighted moments nk, means, Q_k = sum r (x-mu)(x-mu)^H / nk
 (``qce_em_mstep``, FP64 MFMA), and for multi-bit data two more moment passes over transformed copies of
-the observations: the 1-bit signs s = (sign Re x + j sign Im x)/sqrt 2 (Q of s: the arcsine-law
-correlation) and the threshold indicators 1(|Re x| < t) + j 1(|Im x| < t) (their weighted means: the
-per-dimension probabilities the Gauss-Newton variance fit matches), and the per-component Bussgang gains
-(the prepare kernels).  The per-component K x (D x D) corrections (sin law, eigenvalue clipping, the
-scalar Gauss-Newton solves, A Cy A^H with the quantised variances) run on the host in FP64 NumPy, as in
-the reference.  Multi-bit data with non-zero means would need per-component sign / indicator transforms
-of x - mu_k and raises NotImplementedError (the reference script fits zero-mean models,
-Bussgang_GMM_quant.py:47).
+the observations: the 1-bit signs s = (sign Re d + j sign Im d)/sqrt 2 (Q of s: the arcsine-law
+correlation) and the threshold indicators 1(|Re d| < t) + j 1(|Im d| < t) (their weighted means: the
+per-dimension probabilities the Gauss-Newton variance fit matches) of d = x (zero-mean models: transformed
+once per fit) or d = x - mu_k (models with means: per component and M-step, as the reference's diff at :817),
+and the per-component Bussgang gains (the prepare kernels).  The per-component K x (D x D) corrections (sin
+law, eigenvalue clipping, the scalar Gauss-Newton solves, the inverse-EM Sigma update of the Toeplitz types,
+A Cy A^H with the quantised variances) run on the host in FP64 NumPy, as in the reference.
+
+Covariance types: 'full', 'toeplitz' and 'block-toeplitz' (inverse EM) as the reference.  The reference cannot
+complete a fit of 'circulant', 'block-circulant', 'diagonal' or 'spherical' (its M-step helpers for these return
+one array where two are unpacked, :758-762) nor of the Toeplitz types at n_bits = inf (est_cov_from_quant reads
+absent thresholds); ``reference_fit_error`` reproduces those exceptions (tests/golden/quant_fit_struct.npz).
 """
 import warnings
 
@@ -130,6 +134,77 @@ def quant_covariances(Q, nk, reg, n_bits, sigma2, quantizer, moments, gains):
     return cov, cq
 
 
+def quant_covariances_inv(Q, nk, reg, n_bits, sigma2, quantizer, moments, gains, F2, Sigma, prev_covs):
+    """estimate_gaussian_covariances_inv (:880-945): the recovered covariances of the weighted moments Q_k, then the
+    inverse-EM (Barton & Fuhrmann) update of Sigma_k with Cinv = pinv(previous covariances) and
+    C_k = F2^H diag(Sigma_k) F2 + reg I.  Sigma (K, P) is updated in place.  Returns (covariances,
+    covariances_quant)."""
+    K, D, _ = Q.shape
+    eye = np.eye(D)
+    idx = np.arange(D)
+    cov = np.empty_like(Q)
+    cq = np.array(Q, copy=True)
+    Cinv = np.linalg.pinv(np.asarray(prev_covs), hermitian=True)
+    if n_bits == 1:
+        for k in range(K):
+            c = np.sin(np.pi / 2 * cq[k].real) + 1j * np.sin(np.pi / 2 * cq[k].imag)
+            c[idx, idx] += reg
+            cq[k][idx, idx] += reg
+            w, V = np.linalg.eigh(c)
+            w[w < reg] = reg
+            cov[k] = (V * w) @ V.conj().T
+    else:
+        if quantizer is None or quantizer[0] is None:  # est_cov_from_quant reads thresholds.shape (:70)
+            raise AttributeError("'NoneType' object has no attribute 'shape'")
+        corr, probs = moments()
+        for k in range(K):
+            cq[k][idx, idx] += reg
+            c = cov_from_quant(corr[k], probs[k], nk[k], quantizer[0], np.ones(D))  # x0 = 1 here (no x0_vec)
+            c = c - sigma2 * eye
+            c[idx, idx] += reg
+            cov[k] = _eig_clip(c, reg)
+    for k in range(K):
+        theta = np.real(F2 @ (Cinv[k] @ cov[k] @ Cinv[k] - Cinv[k]) @ F2.conj().T)
+        Sigma[k] = Sigma[k] + Sigma[k] ** 2 * np.diag(theta)
+        Sigma[k][Sigma[k] < reg] = reg
+        c = (F2.conj().T * Sigma[k]) @ F2
+        c[idx, idx] += reg
+        cov[k] = c
+    if n_bits > 1:
+        A = gains(cov)
+        for k in range(K):
+            Cy = cov[k] + sigma2 * eye
+            beta = np.clip(np.real(np.mean(A[k])), 0, 1)
+            c = beta ** 2 * Cy
+            c[idx, idx] = quantized_variance(np.real(np.diag(Cy)), quantizer[0], quantizer[1])
+            cq[k] = c
+    return cov, cq
+
+
+def sigma_init(covs, F2, reg):
+    """_initialize's inverse-EM state (:582-586): Sigma_k = Re diag(F2 C_k F2^H), at least reg."""
+    S = np.stack([np.real(np.diag(F2 @ c @ F2.conj().T)) for c in covs])
+    S[S < reg] = reg
+    return S
+
+
+_UNPACK_TYPES = ("circulant", "block-circulant", "diagonal", "spherical")
+
+
+def reference_fit_error(covariance_type, n_components, n_bits):
+    """The exception the reference's Gmm_quant.fit ends in for a covariance type / bit count it cannot fit (see the
+    module docstring), or None.  Pinned to tests/golden/quant_fit_struct.npz."""
+    if covariance_type in _UNPACK_TYPES:
+        if n_components != 2:
+            return ValueError("too many values to unpack (expected 2)")
+        if covariance_type == "spherical":
+            return np.linalg.LinAlgError("0-dimensional array given. Array must be at least two-dimensional")
+        return np.exceptions.AxisError("axis 1 is out of bounds for array of dimension 1")
+    if covariance_type in ("toeplitz", "block-toeplitz") and n_bits == np.inf:
+        return AttributeError("'NoneType' object has no attribute 'shape'")
+    return None
+
+
 class DeviceBackend:
     """The B-sized work of one fit on the device (data and responsibilities stay resident)."""
 
@@ -139,16 +214,21 @@ class DeviceBackend:
         self.n_bits, self.sigma2, self.quantizer, self.quant_type = n_bits, sigma2, quantizer, quant_type
         self.es = self.ez = None
         self.T = 0
-        if n_bits not in (1, np.inf):
-            if not zero_mean:
-                raise NotImplementedError("Gmm_quant.fit: multi-bit covariance recovery with non-zero means "
-                                          "(per-component sign / threshold transforms of x - mu_k) is not provided")
-            S = (np.sign(X.real) + 1j * np.sign(X.imag)) / np.sqrt(2)
-            thr = _positive_thresholds(quantizer[0])
-            self.T = thr.shape[0]
-            Z = np.concatenate([(np.abs(X.real) < t) + 1j * (np.abs(X.imag) < t) for t in thr], axis=1)
-            self.es = _em.DeviceEM(S, K, "full", 0.0, True, device=device)
-            self.ez = _em.DeviceEM(np.ascontiguousarray(Z), K, "diag", 0.0, False, device=device)
+        self.X = X
+        if n_bits not in (1, np.inf) and quantizer is not None and quantizer[0] is not None:
+            self.thr = _positive_thresholds(quantizer[0])
+            self.T = self.thr.shape[0]
+            if zero_mean:  # d = x for every component: transform once
+                S, Z = self._transforms(X)
+                self.es = _em.DeviceEM(S, K, "full", 0.0, True, device=device)
+                self.ez = _em.DeviceEM(Z, K, "diag", 0.0, False, device=device)
+
+    def _transforms(self, D):
+        """1-bit signs of D and the threshold indicators 1(|Re D| < t) + j 1(|Im D| < t), t = the positive
+        thresholds (cov_est_quant.py:42-43, :60-63)."""
+        S = (np.sign(D.real) + 1j * np.sign(D.imag)) / np.sqrt(2)
+        Z = np.concatenate([(np.abs(D.real) < t) + 1j * (np.abs(D.imag) < t) for t in self.thr], axis=1)
+        return np.ascontiguousarray(S), np.ascontiguousarray(Z)
 
     def estep(self, means, covs_quant, weights):
         return self.em.estep(means, covs_quant, weights)
@@ -157,10 +237,28 @@ class DeviceBackend:
         nk, means, cov = self.em.mstep(resp=resp, reg=0.0)
         return nk, means, cov
 
-    def moments(self, resp=None):
+    def moments(self, resp=None, means=None):
+        """(corr (K, D, D), probs (K, D, T, 2)) of d = x (means None) or d = x - mu_k (per component)."""
         R = self.em.R if resp is None else resp
-        _, _, corr = self.es.mstep(resp=R)
-        _, pz, _ = self.ez.mstep(resp=R)
+        if means is None:
+            _, _, corr = self.es.mstep(resp=R)
+            _, pz, _ = self.ez.mstep(resp=R)
+        else:
+            import torch
+            K = self.K
+            corr, pz = [], []
+            for k in range(K):
+                Rk = R[:, k:k + 1].contiguous() if isinstance(R, torch.Tensor) else np.ascontiguousarray(R[:, k:k + 1])
+                S, Z = self._transforms(self.X - means[k])
+                es = _em.DeviceEM(S, 1, "full", 0.0, True, device=self.device)
+                ez = _em.DeviceEM(Z, 1, "diag", 0.0, False, device=self.device)
+                try:
+                    corr.append(es.mstep(resp=Rk)[2][0])
+                    pz.append(ez.mstep(resp=Rk)[1][0])
+                finally:
+                    es.close()
+                    ez.close()
+            corr, pz = np.stack(corr), np.stack(pz)
         K, D = corr.shape[0], corr.shape[1]
         pz = pz.reshape(K, self.T, D)  # (K, T, D): real part = Re-indicator mean, imaginary = Im-indicator
         probs = np.stack([np.real(pz), np.imag(pz)], axis=-1).transpose(0, 2, 1, 3)  # (K, D, T, 2)
@@ -191,11 +289,18 @@ class DeviceBackend:
                 e.close()
 
 
-def estimate_parameters(obj, be, resp=None):
-    """estimate_gaussian_parameters (:732-771) for 'full': nk, means, covariances; sets covariances_quant."""
+def estimate_parameters(obj, be, resp=None, inv=False):
+    """estimate_gaussian_parameters (:732-771): nk, means, covariances ('full' branch, or 'inv-em' for the Toeplitz
+    types after the initialisation); sets covariances_quant."""
     nk, means, Q = be.mstep(resp)
-    cov, cq = quant_covariances(Q, nk, obj.gm.reg_covar, obj.n_bits, obj.sigma2, obj.quantizer,
-                                lambda: be.moments(resp), be.gains)
+    centred = None if obj.params.get("zero_mean", False) else means
+    moments = lambda: be.moments(resp, centred)  # noqa: E731
+    if inv:
+        cov, cq = quant_covariances_inv(Q, nk, obj.gm.reg_covar, obj.n_bits, obj.sigma2, obj.quantizer, moments,
+                                        be.gains, obj.F2, obj.gm.Sigma, obj.gm.covariances_)
+    else:
+        cov, cq = quant_covariances(Q, nk, obj.gm.reg_covar, obj.n_bits, obj.sigma2, obj.quantizer, moments,
+                                    be.gains)
     obj.covariances_quant = cq
     return nk, means, cov
 
@@ -212,6 +317,9 @@ def fit_predict(obj, X, backend=None):
         raise ValueError("Unimplemented initialization method '%s'" % gm.init_params)
     K = gm.n_components
     zero_mean = bool(obj.params.get("zero_mean", False))
+    inv = "inv-em" in obj.params
+    if inv and obj.n_bits != 1 and (obj.quantizer is None or obj.quantizer[0] is None):
+        raise AttributeError("'NoneType' object has no attribute 'shape'")  # the reference's first M-step
     be = backend or DeviceBackend(X, K, gm.reg_covar, zero_mean, obj.n_bits, obj.sigma2, obj.quantizer,
                                   obj.quant_type, obj.device)
     do_init = not (gm.warm_start and hasattr(obj, "converged_"))
@@ -237,11 +345,13 @@ def fit_predict(obj, X, backend=None):
                 gm.weights_ = nk / n_samples if gm.weights_init is None else gm.weights_init
                 gm.means_ = means if gm.means_init is None else gm.means_init
                 gm.covariances_ = cov
+                if inv:
+                    gm.Sigma = sigma_init(cov, obj.F2, gm.reg_covar)
             lower_bound = -np.inf if do_init else gm.lower_bound_
             for n_iter in range(1, gm.max_iter + 1):
                 prev_lower_bound = lower_bound
                 log_prob_norm = be.estep(gm.means_, obj.covariances_quant, gm.weights_)
-                nk, means, cov = estimate_parameters(obj, be)
+                nk, means, cov = estimate_parameters(obj, be, inv=inv)
                 gm.weights_, gm.means_, gm.covariances_ = nk / n_samples, means, cov
                 lower_bound = log_prob_norm
                 print(f"Iteration {n_iter}/{gm.max_iter} | lower bound: {lower_bound}")

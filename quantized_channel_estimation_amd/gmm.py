@@ -450,21 +450,38 @@ class Gmm_quant(Gmm_nbit):
         self.eval_mode = False
         self.precisions_cholesky_quant = None
 
-    def fit(self, h, n_bits, sigma2, quantizer, quant_type, blocks=None, zero_mean=False):
-        """EM on quantised observations with covariance recovery (gmm_cplx_quant.py:103-189, 'full'
-        branch :155-159): device E-step on covariances_quant and device moments, the recovery algebra on the
-        host (_em_quant.py).  Other covariance types raise NotImplementedError."""
+    def fit(self, h, n_bits, sigma2, quantizer, quant_type, blocks=None, zero_mean=False, _backend=None):
+        """EM on quantised observations with covariance recovery (gmm_cplx_quant.py:103-189): 'full' (:155-159) and
+        the inverse-EM 'toeplitz' / 'block-toeplitz' (:160-181, with the partial DFT F2), zero mean or with means;
+        device E-step on covariances_quant and device moments, the recovery algebra on the host (_em_quant.py).
+        The covariance types the reference cannot fit end in the reference's own exception
+        (_em_quant.reference_fit_error)."""
         from . import _em_quant
         _drop_pending(self.gm)
         self.params["zero_mean"] = bool(zero_mean)
         self.n_bits, self.sigma2, self.quantizer, self.quant_type = n_bits, sigma2, quantizer, quant_type
-        if self.gm.covariance_type != "full":
-            raise NotImplementedError(f"Gmm_quant.fit on the device covers covariance_type 'full', not "
-                                      f"{self.gm.covariance_type!r}")
+        ct = self.gm.covariance_type
+        err = _em_quant.reference_fit_error(ct, self.gm.n_components, n_bits)
+        if err is not None:
+            raise err
+        if ct == "toeplitz":  # :166-172
+            self.params["inv-em"] = True
+            self.gm.covariance_type = "full"
+            n_1 = np.asarray(h).shape[1]
+            self.F2 = np.fft.fft(np.eye(2 * n_1))[:, :n_1] / np.sqrt(2 * n_1)
+        elif ct == "block-toeplitz":  # :173-181
+            self.params["inv-em"] = True
+            self.gm.covariance_type = "full"
+            n_1, n_2 = blocks
+            F2_1 = np.fft.fft(np.eye(2 * n_1))[:, :n_1] / np.sqrt(2 * n_1)
+            F2_2 = np.fft.fft(np.eye(2 * n_2))[:, :n_2] / np.sqrt(2 * n_2)
+            self.F2 = np.kron(F2_1, F2_2)
+        elif ct != "full":
+            raise NotImplementedError(f"Fitting for covariance_type = {ct} is not implemented.")
         self._dev = None
         self._dev_key = None
         self._state = None
-        _em_quant.fit_predict(self, np.asarray(h))
+        _em_quant.fit_predict(self, np.asarray(h), backend=_backend)  # _backend: tests' CPU stand-in
         self.means_cplx = self.gm.means_.copy()
         self.covs_cplx = self.gm.covariances_.copy()
         self.chol = self.gm.precisions_cholesky_.copy()
