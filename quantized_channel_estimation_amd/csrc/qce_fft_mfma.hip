@@ -7,10 +7,12 @@
 // result keeps the FP64 accuracy of the reference (gmm_cplx_bussgang.py computes in complex128).
 //
 // Workgroup = 4 waves and TS = 4096 / N observations (64 for N <= 64): the tile of spectra (TS x N
-// complex128 = 64 KB) sits in LDS, two workgroups per CU.  Wave w owns 16 observations (MFMA columns)
-// and a range of NB = min(N, 64) bins: for N > 64 the KW = N / 64 waves of one observation group
-// split the bins and add their partial log-probabilities through LDS (fixed order, so every wave sees
-// bit-identical lp).  Components stream in blocks of 16 (MFMA rows) with an online softmax:
+// complex128 = 64 KB) sits in LDS for the transforms, two workgroups per CU.  Wave w owns 16 observations
+// (MFMA columns) and a range of NB = min(N, 64) bins, whose spectra (and |Y|^2) it keeps in registers through
+// the component loop: for N > 64 the KW = N / 64 waves of one observation group split the bins and add their
+// partial log-probabilities through LDS in a fixed order (every wave sees bit-identical lp), double-buffered in
+// the then unused spectra tile with one barrier per block, the next block's lp MFMAs in flight behind the
+// exchange and softmax of the current one.  Components stream in blocks of 16 (MFMA rows) with an online softmax:
 //   lp block   D[comp][obs]  = sum_bins (-rinv)[bin][comp] * |Y|^2[bin][obs]       (A: table, B: LDS)
 //   filter     F[bin][obs]  += w[comp][bin] * e^{lp - m}[comp][obs]                (B: the lp tile as is)
 // The f64 D layout (row = lane/16 + 4 r, col = lane % 16) is exactly the B-operand layout of k-step r
@@ -135,7 +137,7 @@ QCE_DEV void fft_axis_passes(double2* T, int lgTS, int RS, int lgN, int lgL, int
 }
 
 template <int N, int OUT, bool has_mean>
-__global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int lg2, int Kp,
+__global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B, int lg1, int lg2, int Kp,
                                                      const double2* __restrict__ y, const double* __restrict__ pr,
                                                      const double* __restrict__ pur, const double* __restrict__ pui,
                                                      const double* __restrict__ pc, const double* __restrict__ pw,
@@ -152,7 +154,6 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double2* tw = reinterpret_cast<double2*>(smem);
   double2* T = tw + 128;
-  double* X = reinterpret_cast<double*>(T + TS * RS);  // KW > 1: partial lp tiles [SG][KW][4][64]
   const int tid = threadIdx.x;
   const long long b0 = (long long)blockIdx.x * TS;
   const int rows = (int)((B - b0) < TS ? (B - b0) : TS);
@@ -190,6 +191,19 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
   const int srow = sg * 16 + col;
   double2* Trow = T + srow * RS;
   const int bin0 = kw * NB;
+  // The lane's spectrum values stay in registers for the whole component loop: bins bin0 + 4 u + hq (u < NB / 4)
+  // are the lp product's B operand of k-step u and, as u = 4 t + r, the filter accumulator's row hq + 4 r of
+  // tile t -- so the spectra tile is free during the loop and carries the lp exchange (double-buffered).
+  constexpr int NU = NB / 4;
+  constexpr int NP2 = has_mean ? 1 : NU;  // |Y|^2 kept (zero mean) or recomputed per block (the mean variant's
+                                          // extra accumulators take those registers)
+  double2 yv[NU];
+  double p2[NP2];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    yv[u] = Trow[bin0 + 4 * u + hq];
+    if constexpr (!has_mean) p2[u] = yv[u].x * yv[u].x + yv[u].y * yv[u].y;
+  }
   constexpr int NTM = has_mean ? NT : 1;
   f64x4 F[NT], Br[NTM], Bi[NTM];
 #pragma unroll
@@ -200,60 +214,58 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
     for (int r = 0; r < 4; ++r) Br[t][r] = Bi[t][r] = 0.0;
   double m = -__builtin_inf(), ssum = 0.0;
   const int ncb = Kp >> 4;
-  // zero-mean models: the table operands of block cb+1 are fetched while block cb computes (registers to
-  // spare); the mean variants load them in place
-  constexpr bool PF = !has_mean;
-  constexpr int NA = PF ? NB / 4 : 1, NWF = PF ? 4 * NT : 1;
-  double ca[NA], cw[NWF];
-  auto fetch = [&](int cb, double* a, double* w) {
+  // lp partial of component block cb over this wave's bins: D[comp][obs] = c'_comp (wave 0) - sum |Y|^2 rinv
+  // (+ 2 Re conj(Y) u with means); table operands straight from L2 (the next block's are issued while this
+  // block's softmax and filter run)
+  auto lp_partial = [&](int cb) -> f64x4 {
     const int c0 = cb << 4;
-    const double* pa = pr + (long long)(bin0 + hq) * Kp + c0 + col;
-#pragma unroll
-    for (int t = 0; t < NA; ++t) a[t] = pa[(long long)4 * t * Kp];
-#pragma unroll
-    for (int r = 0; r < 4 && PF; ++r)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) w[r * NT + t] = pw[(long long)(c0 + hq + 4 * r) * N + bin0 + col + 16 * t];
-  };
-  if constexpr (PF) fetch(0, ca, cw);
-  for (int cb = 0; cb < ncb; ++cb) {
-    const int c0 = cb << 4;
-    double na[NA], nw[NWF];
-    if constexpr (PF) fetch(cb + 1 < ncb ? cb + 1 : cb, na, nw);
     f64x4 C;
 #pragma unroll
     for (int r = 0; r < 4; ++r) C[r] = (kw == 0) ? pc[c0 + hq + 4 * r] : 0.0;
-    {
-      const long long o = (long long)(bin0 + hq) * Kp + c0 + col;
-      const double* pa = pr + o;
+    const long long o = (long long)(bin0 + hq) * Kp + c0 + col;
+    const double* pa = pr + o;
+    if constexpr (!has_mean) {
+      double a[NU];
 #pragma unroll
-      for (int t = 0; t < NB / 4; ++t) {
-        const double2 v = Trow[bin0 + 4 * t + hq];
-        C = mfma16x16x4d(PF ? ca[PF ? t : 0] : pa[(long long)4 * t * Kp], v.x * v.x + v.y * v.y, C);
-      }
-      if constexpr (has_mean) {
-        const double *qa = pur + o, *qb = pui + o;
+      for (int u = 0; u < NU; ++u) a[u] = pa[(long long)4 * u * Kp];
 #pragma unroll
-        for (int t = 0; t < NB / 4; ++t) {
-          const double2 v = Trow[bin0 + 4 * t + hq];
-          C = mfma16x16x4d(qa[(long long)4 * t * Kp], v.x, C);
-          C = mfma16x16x4d(qb[(long long)4 * t * Kp], v.y, C);
-        }
+      for (int u = 0; u < NU; ++u) C = mfma16x16x4d(a[u], p2[u], C);
+    } else {
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+        C = mfma16x16x4d(pa[(long long)4 * u * Kp], yv[u].x * yv[u].x + yv[u].y * yv[u].y, C);
+    }
+    if constexpr (has_mean) {
+      const double *qa = pur + o, *qb = pui + o;
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        C = mfma16x16x4d(qa[(long long)4 * u * Kp], yv[u].x, C);
+        C = mfma16x16x4d(qb[(long long)4 * u * Kp], yv[u].y, C);
       }
     }
-    if constexpr (KW > 1) {  // add the bin-range partials of the KW waves of this observation group
-      double* xs = X + (sg * KW + kw) * 256 + lane;
+    return C;
+  };
+  double* X = reinterpret_cast<double*>(T);  // [2][SG][KW][4][64] lp partials, aliasing the spectra tile
+  auto xslot = [&](int buf, int q) -> double* { return X + (((buf * SG + sg) * KW + q) * 256); };
+  __syncthreads();  // every wave holds its spectra: the tile may now carry the exchange
+  f64x4 Cn = lp_partial(0);
+  if constexpr (KW > 1) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) xs[r * 64] = C[r];
-      __syncthreads();
+    for (int r = 0; r < 4; ++r) xslot(0, kw)[r * 64 + lane] = Cn[r];
+  }
+  for (int cb = 0; cb < ncb; ++cb) {
+    const int c0 = cb << 4;
+    f64x4 C = Cn;
+    if constexpr (KW > 1) __syncthreads();  // block cb's partials are in X[cb & 1]; X[(cb + 1) & 1] is free
+    if (cb + 1 < ncb) Cn = lp_partial(cb + 1);  // MFMAs in flight behind the exchange and softmax of block cb
+    if constexpr (KW > 1) {  // add the KW bin-range partials of this observation group, fixed order
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        double acc = X[(sg * KW) * 256 + r * 64 + lane];
+        double acc = xslot(cb & 1, 0)[r * 64 + lane];
 #pragma unroll
-        for (int q = 1; q < KW; ++q) acc += X[(sg * KW + q) * 256 + r * 64 + lane];
+        for (int q = 1; q < KW; ++q) acc += xslot(cb & 1, q)[r * 64 + lane];
         C[r] = acc;
       }
-      __syncthreads();
     }
     // online softmax over this block of 16 components (rows hq + 4 r of the tile, all 4 lane groups)
     double bm = fmax(fmax(C[0], C[1]), fmax(C[2], C[3]));
@@ -282,13 +294,18 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
         Bi[t] *= alpha;
       }
     }
+    // filter: F[bin][obs] += w[comp][bin] e[comp][obs] (the lp D layout is the B layout of k-step r)
+    double wv[4][NT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) wv[r][t] = pw[(long long)(c0 + hq + 4 * r) * N + bin0 + col + 16 * t];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const long long o = (long long)(c0 + hq + 4 * r) * N + bin0 + col;
-      const double* wa = pw + o;
 #pragma unroll
-      for (int t = 0; t < NT; ++t) F[t] = mfma16x16x4d(PF ? cw[PF ? r * NT + t : 0] : wa[16 * t], e[r], F[t]);
+      for (int t = 0; t < NT; ++t) F[t] = mfma16x16x4d(wv[r][t], e[r], F[t]);
       if constexpr (has_mean) {
+        const long long o = (long long)(c0 + hq + 4 * r) * N + bin0 + col;
         const double *ba = pbr + o, *bb = pbi + o;
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
@@ -297,21 +314,23 @@ __global__ __launch_bounds__(256, 2) void k_fft_mfma(long long B, int lg1, int l
         }
       }
     }
-    if constexpr (PF) {
+    if constexpr (KW > 1) {
+      if (cb + 1 < ncb) {
 #pragma unroll
-      for (int t = 0; t < NA; ++t) ca[t] = na[t];
-#pragma unroll
-      for (int t = 0; t < NWF; ++t) cw[t] = nw[t];
+        for (int r = 0; r < 4; ++r) xslot((cb + 1) & 1, kw)[r * 64 + lane] = Cn[r];
+      }
     }
   }
-  // Z = Y f + bb in place (each (observation, bin) of the tile belongs to exactly one lane)
+  if constexpr (KW > 1) __syncthreads();  // every wave is done with the exchange: the tile takes Z
+  // Z = Y f + bb (each (observation, bin) of the tile belongs to exactly one lane)
   const double sc = (OUT == 0) ? 1.0 / ssum : 1.0;
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int bin = bin0 + 16 * t + hq + 4 * r;
-      const double2 v = Trow[bin];
+      const int u = 4 * t + r;
+      const int bin = bin0 + 4 * u + hq;
+      const double2 v = yv[u];
       const double f = F[t][r] * sc;
       if constexpr (has_mean)
         Trow[bin] = make_double2(fma(v.x, f, Br[t][r] * sc), fma(v.y, f, Bi[t][r] * sc));
@@ -806,7 +825,9 @@ template <int N, int OUT, bool HM>
 hipError_t launch_mfma_t(const QceFftEstArgs& a, hipStream_t st) {
   constexpr int KW = N >= 64 ? N / 64 : 1;
   constexpr int TS = 16 * (4 / KW);
-  const size_t lds = 128 * 16 + (size_t)TS * (N + 1) * 16 + (KW > 1 ? (size_t)(4 / KW) * KW * 256 * 8 : 0);
+  // twiddles + the spectra tile (the lp exchange of the component loop aliases the tile)
+  const size_t lds = 128 * 16 + (size_t)TS * (N + 1) * 16;
+  static_assert(2 * 4 * 256 * 8 <= TS * (N + 1) * 16, "exchange fits the tile");
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)k_fft_mfma<N, OUT, HM>, hipFuncAttributeMaxDynamicSharedMemorySize,
