@@ -195,15 +195,9 @@ __global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B,
   // are the lp product's B operand of k-step u and, as u = 4 t + r, the filter accumulator's row hq + 4 r of
   // tile t -- so the spectra tile is free during the loop and carries the lp exchange (double-buffered).
   constexpr int NU = NB / 4;
-  constexpr int NP2 = has_mean ? 1 : NU;  // |Y|^2 kept (zero mean) or recomputed per block (the mean variant's
-                                          // extra accumulators take those registers)
   double2 yv[NU];
-  double p2[NP2];
 #pragma unroll
-  for (int u = 0; u < NU; ++u) {
-    yv[u] = Trow[bin0 + 4 * u + hq];
-    if constexpr (!has_mean) p2[u] = yv[u].x * yv[u].x + yv[u].y * yv[u].y;
-  }
+  for (int u = 0; u < NU; ++u) yv[u] = Trow[bin0 + 4 * u + hq];
   constexpr int NTM = has_mean ? NT : 1;
   f64x4 F[NT], Br[NTM], Bi[NTM];
 #pragma unroll
@@ -214,28 +208,25 @@ __global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B,
     for (int r = 0; r < 4; ++r) Br[t][r] = Bi[t][r] = 0.0;
   double m = -__builtin_inf(), ssum = 0.0;
   const int ncb = Kp >> 4;
+  // Table operands come straight from L2 with one block of prefetch distance: the lp operands of block cb + 2 are
+  // issued in iteration cb (consumed by the lp MFMAs of cb + 2, which run in iteration cb + 1), the filter
+  // operands of block cb at the top of iteration cb (consumed after the exchange and softmax).
+  auto load_lp = [&](int cb, double (&a)[NU]) {
+    const double* pa = pr + (long long)(bin0 + hq) * Kp + (cb << 4) + col;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) a[u] = pa[(long long)4 * u * Kp];
+  };
   // lp partial of component block cb over this wave's bins: D[comp][obs] = c'_comp (wave 0) - sum |Y|^2 rinv
-  // (+ 2 Re conj(Y) u with means); table operands straight from L2 (the next block's are issued while this
-  // block's softmax and filter run)
-  auto lp_partial = [&](int cb) -> f64x4 {
+  // (+ 2 Re conj(Y) u with means)
+  auto lp_partial = [&](int cb, const double (&a)[NU]) -> f64x4 {
     const int c0 = cb << 4;
     f64x4 C;
 #pragma unroll
     for (int r = 0; r < 4; ++r) C[r] = (kw == 0) ? pc[c0 + hq + 4 * r] : 0.0;
-    const long long o = (long long)(bin0 + hq) * Kp + c0 + col;
-    const double* pa = pr + o;
-    if constexpr (!has_mean) {
-      double a[NU];
 #pragma unroll
-      for (int u = 0; u < NU; ++u) a[u] = pa[(long long)4 * u * Kp];
-#pragma unroll
-      for (int u = 0; u < NU; ++u) C = mfma16x16x4d(a[u], p2[u], C);
-    } else {
-#pragma unroll
-      for (int u = 0; u < NU; ++u)
-        C = mfma16x16x4d(pa[(long long)4 * u * Kp], yv[u].x * yv[u].x + yv[u].y * yv[u].y, C);
-    }
+    for (int u = 0; u < NU; ++u) C = mfma16x16x4d(a[u], yv[u].x * yv[u].x + yv[u].y * yv[u].y, C);
     if constexpr (has_mean) {
+      const long long o = (long long)(bin0 + hq) * Kp + c0 + col;
       const double *qa = pur + o, *qb = pui + o;
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
@@ -247,8 +238,11 @@ __global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B,
   };
   double* X = reinterpret_cast<double*>(T);  // [2][SG][KW][4][64] lp partials, aliasing the spectra tile
   auto xslot = [&](int buf, int q) -> double* { return X + (((buf * SG + sg) * KW + q) * 256); };
+  double la[NU];
+  load_lp(0, la);
   __syncthreads();  // every wave holds its spectra: the tile may now carry the exchange
-  f64x4 Cn = lp_partial(0);
+  f64x4 Cn = lp_partial(0, la);
+  if (ncb > 1) load_lp(1, la);
   if constexpr (KW > 1) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) xslot(0, kw)[r * 64 + lane] = Cn[r];
@@ -257,7 +251,15 @@ __global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B,
     const int c0 = cb << 4;
     f64x4 C = Cn;
     if constexpr (KW > 1) __syncthreads();  // block cb's partials are in X[cb & 1]; X[(cb + 1) & 1] is free
-    if (cb + 1 < ncb) Cn = lp_partial(cb + 1);  // MFMAs in flight behind the exchange and softmax of block cb
+    double wv[4][NT];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int t = 0; t < NT; ++t) wv[r][t] = pw[(long long)(c0 + hq + 4 * r) * N + bin0 + col + 16 * t];
+    if (cb + 1 < ncb) {
+      Cn = lp_partial(cb + 1, la);  // MFMAs in flight behind the exchange and softmax of block cb
+      if (cb + 2 < ncb) load_lp(cb + 2, la);
+    }
     if constexpr (KW > 1) {  // add the KW bin-range partials of this observation group, fixed order
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -295,11 +297,6 @@ __global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B,
       }
     }
     // filter: F[bin][obs] += w[comp][bin] e[comp][obs] (the lp D layout is the B layout of k-step r)
-    double wv[4][NT];
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-#pragma unroll
-      for (int t = 0; t < NT; ++t) wv[r][t] = pw[(long long)(c0 + hq + 4 * r) * N + bin0 + col + 16 * t];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
 #pragma unroll
