@@ -136,6 +136,29 @@ QCE_DEV void fft_axis_passes(double2* T, int lgTS, int RS, int lgN, int lgL, int
   }
 }
 
+// Diagnostic build only (-DQCE_STAMPS): per-wave cycle sums of k_fft_wave's / k_fft_mfma's segments (s_memtime) into
+// g_fft_stamps (qce_debug_fft_stamps); the product kernel executes no stamp.
+#ifdef QCE_STAMPS
+__device__ unsigned long long* g_fft_stamps = nullptr;
+#define FW_STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime();
+#define FW_STAMP(i)                                             \
+  do {                                                          \
+    __builtin_amdgcn_sched_barrier(0);                          \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          \
+    st_acc[(i)] += t_ - st_prev;                                \
+    st_prev = t_;                                               \
+    __builtin_amdgcn_sched_barrier(0);                          \
+  } while (0)
+#define FW_STAMP_FLUSH                                                                                  \
+  if (g_fft_stamps && lane == 0 && blockIdx.x < 4096)                                                  \
+    for (int i_ = 0; i_ < 8; ++i_) g_fft_stamps[((long long)blockIdx.x * 4 + wid) * 8 + i_] = st_acc[i_];
+#else
+#define FW_STAMP_DECL
+#define FW_STAMP(i)
+#define FW_STAMP_FLUSH
+#endif
+
 template <int N, int OUT, bool has_mean>
 __global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B, int lg1, int lg2, int Kp,
                                                      const double2* __restrict__ y, const double* __restrict__ pr,
@@ -157,6 +180,7 @@ __global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B,
   const int tid = threadIdx.x;
   const long long b0 = (long long)blockIdx.x * TS;
   const int rows = (int)((B - b0) < TS ? (B - b0) : TS);
+  FW_STAMP_DECL
 
   for (int t = tid; t < 128; t += 256) {
     double sn, cs;
@@ -181,9 +205,11 @@ __global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B,
     }
   }
   __syncthreads();
+  FW_STAMP(0);
   const int n1 = 1 << lg1, n2 = 1 << lg2;
   fft_axis_passes<false>(T, lgTS, RS, lgN, lg2, 1, tw);
   if (lg1 > 0) fft_axis_passes<false>(T, lgTS, RS, lgN, lg1, n2, tw);
+  FW_STAMP(1);
 
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int sg = wid % SG, kw = wid / SG;
@@ -243,6 +269,7 @@ __global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B,
   __syncthreads();  // every wave holds its spectra: the tile may now carry the exchange
   f64x4 Cn = lp_partial(0, la);
   if (ncb > 1) load_lp(1, la);
+  FW_STAMP(2);
   if constexpr (KW > 1) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) xslot(0, kw)[r * 64 + lane] = Cn[r];
@@ -318,6 +345,7 @@ __global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B,
       }
     }
   }
+  FW_STAMP(3);
   if constexpr (KW > 1) __syncthreads();  // every wave is done with the exchange: the tile takes Z
   // Z = Y f + bb (each (observation, bin) of the tile belongs to exactly one lane)
   const double sc = (OUT == 0) ? 1.0 / ssum : 1.0;
@@ -338,10 +366,12 @@ __global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B,
     om[b0 + srow] = m;
     os[b0 + srow] = ssum;
   }
+  FW_STAMP(4);
   __syncthreads();
   if (lg1 > 0) fft_axis_passes<true>(T, lgTS, RS, lgN, lg1, n2, tw);
   fft_axis_passes<true>(T, lgTS, RS, lgN, lg2, 1, tw);
   (void)n1;
+  FW_STAMP(5);
   if (OUT == 3) {
     float2* at = reinterpret_cast<float2*>(oa) + b0 * N;
 #pragma unroll 4
@@ -349,16 +379,12 @@ __global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B,
       const double2 v = T[(e >> lgN) * RS + (e & (N - 1))];
       at[e] = make_float2((float)v.x, (float)v.y);
     }
-    return;
-  }
-  if (OUT == 4) {  // FP64 accumulator of the K-shard partial (qce_estimate_partial_f64)
+  } else if (OUT == 4) {  // FP64 accumulator of the K-shard partial (qce_estimate_partial_f64)
     double2* at = reinterpret_cast<double2*>(oa) + b0 * N;
 #pragma unroll 4
     for (int e = tid; e < rows * N; e += 256) at[e] = T[(e >> lgN) * RS + (e & (N - 1))];
-    return;
-  }
-  double2* ht = h + b0 * N;
-  if (rows == TS) {  // whole tile: all LDS reads issued before the unguarded stores
+  } else if (rows == TS) {  // whole tile: all LDS reads issued before the unguarded stores
+    double2* ht = h + b0 * N;
     constexpr int NL = TS * N / 256;
     double2 v[NL];
 #pragma unroll
@@ -368,34 +394,15 @@ __global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B,
     }
 #pragma unroll
     for (int i = 0; i < NL; ++i) ht[tid + 256 * i] = v[i];
-    return;
-  }
+  } else {
+    double2* ht = h + b0 * N;
 #pragma unroll 4
-  for (int e = tid; e < rows * N; e += 256) ht[e] = T[(e >> lgN) * RS + (e & (N - 1))];
+    for (int e = tid; e < rows * N; e += 256) ht[e] = T[(e >> lgN) * RS + (e & (N - 1))];
+  }
+  FW_STAMP(6);
+  FW_STAMP_FLUSH
 }
 
-// Diagnostic build only (-DQCE_STAMPS): per-wave cycle sums of k_fft_wave's segments (s_memtime) into
-// g_fft_stamps (qce_debug_fft_stamps); the product kernel executes no stamp.
-#ifdef QCE_STAMPS
-__device__ unsigned long long* g_fft_stamps = nullptr;
-#define FW_STAMP_DECL unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = __builtin_amdgcn_s_memtime();
-#define FW_STAMP(i)                                             \
-  do {                                                          \
-    __builtin_amdgcn_sched_barrier(0);                          \
-    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          \
-    st_acc[(i)] += t_ - st_prev;                                \
-    st_prev = t_;                                               \
-    __builtin_amdgcn_sched_barrier(0);                          \
-  } while (0)
-#define FW_STAMP_FLUSH                                                                                  \
-  if (g_fft_stamps && lane == 0)                                                                        \
-    for (int i_ = 0; i_ < 8; ++i_) g_fft_stamps[((long long)blockIdx.x * 4 + wid) * 8 + i_] = st_acc[i_];
-#else
-#define FW_STAMP_DECL
-#define FW_STAMP(i)
-#define FW_STAMP_FLUSH
-#endif
 
 // Reductions over the four 16-lane rows of a wave (lanes l, l^16, l^32, l^48) on the gfx950 cross-row
 // swaps (no LDS round trip): op(swap pair) = op(x[l], x[l^16]) in either operand order, so every row of a

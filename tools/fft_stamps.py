@@ -41,7 +41,7 @@ def main():
     st = buf[:n].reshape(-1, 8).astype(np.float64)
     st = st[st.sum(1) > 0]
     tot = st.sum(1)
-    names = ["y load", "FFT fwd", "y2+lp0", "loop", "last+Z", "FFT inv", "store", "-"]
+    names = ["y load", "FFT fwd", "y2+lp0", "loop", "last+Z", "FFT inv", "store", "-"]  # k_fft_mfma: Y regs + lp0, loop, Z
     print(f"waves {st.shape[0]}, mean cycles/wave {tot.mean():.4g} (min {tot.min():.4g}, max {tot.max():.4g})")
     for i in range(7):
         print(f"  {names[i]:8s} {st[:, i].mean() / tot.mean():.4f}  mean {st[:, i].mean():.4g} cycles/wave")
