@@ -73,7 +73,10 @@ def parse():
                     help="K-shard SUM collective: reduce-scatter (rank keeps its rows) or all-reduce")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline budget per leg (0 = skip)")
     ap.add_argument("--no-parity", action="store_true")
-    ap.add_argument("--no-extras", action="store_true", help="skip the fast-path and drop-in side lines")
+    ap.add_argument("--no-extras", action="store_true", help="skip the fast-path side line")
+    ap.add_argument("--dropin", action="store_true",
+                    help="add the drop-in (numpy host I/O) side line; off by default because its chunked launches of "
+                         "the headline kernel would enter a rocprof kernel-stats average of the bench command")
     ap.add_argument("--launch-check", action="store_true",
                     help="CPU rehearsal of the launcher: ranks rendezvous over gloo, barrier + MAX-over-ranks "
                          "timing, rank 0 prints one JSON line; no GPU is touched")
@@ -523,7 +526,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras and args.config == "metric":
         extras["fast_path"] = fast_line(cfg, means, covs, w, yd, out, stream, max(3, args.steps // 2), qargs, ho,
                                         n_chk)
-        extras["dropin"] = dropin_line(cfg, means, covs, w, y, quantizer)
+        if args.dropin:
+            extras["dropin"] = dropin_line(cfg, means, covs, w, y, quantizer)
     if rank == 0:
         line = {
             "metric": METRIC,
