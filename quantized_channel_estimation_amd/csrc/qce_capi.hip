@@ -120,6 +120,7 @@ struct qce_model {
   DevBuf<int> f_bad;
   DevBuf<double> f_pr, f_pur, f_pui, f_pc, f_pw, f_pbr, f_pbi;  // qce_fft_mfma.hip tables
   int fft_mfma = 0;                                            // the MFMA kernel serves 'all' / partial
+  int fft_chunk = 1;  // zero-mean N = 128, 256: k_fft_chunk (fragment-order tables); 0: k_fft_mfma (QCE_FFT_CHUNK=0)
   // host-I/O pipeline of qce_estimate: two pinned slots per direction, copy-in / copy-out streams
   struct {
     double2* pin_y[2] = {nullptr, nullptr};
@@ -502,6 +503,7 @@ QceFftEstArgs fft_args(qce_model* m, const double2* y, long long B) {
   a.pbr = m->f_pbr.p;
   a.pbi = m->f_pbi.p;
   a.cu = m->cu_count;
+  a.chunk = m->fft_chunk;
   return a;
 }
 
@@ -822,6 +824,10 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
     fa.status = m->status.p;
     HIPCHK(qce_launch_fft_prep(fa, st));
     m->fft_mfma = 0;
+    {
+      const char* e = getenv("QCE_FFT_CHUNK");  // read per prepare: the table order and the kernel go together
+      m->fft_chunk = !(e && e[0] == '0');
+    }
     if (qce_fft_mfma_shape(N) && fft_mfma_enabled()) {
       const size_t KpN = (size_t)qce_fft_kpad(K) * N;
       HIPCHK(m->f_pr.ensure(KpN));

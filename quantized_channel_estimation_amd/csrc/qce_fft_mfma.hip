@@ -403,7 +403,6 @@ __global__ __launch_bounds__(256, has_mean ? 1 : 2) void k_fft_mfma(long long B,
   FW_STAMP_FLUSH
 }
 
-
 // Reductions over the four 16-lane rows of a wave (lanes l, l^16, l^32, l^48) on the gfx950 cross-row
 // swaps (no LDS round trip): op(swap pair) = op(x[l], x[l^16]) in either operand order, so every row of a
 // column gets bit-identical results.
@@ -754,10 +753,265 @@ __global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wave(long long B, long 
   FW_STAMP_FLUSH
 }
 
+// Zero-mean models, N = 128, 256: one workgroup (4 waves) per 16 observations, the components split over the waves
+// for the log-probabilities and the bins split over the waves for the filter, so the softmax of every (component,
+// observation) is evaluated exactly once and the waves meet at two barriers per chunk of 128 components (not per
+// block of 16).  Per chunk:
+//   lp    wave w: blocks w, w + 4 of the chunk over all N bins: D[comp][obs] = c'_comp + sum_bins (-rinv) |Y|^2
+//         (A: fragment-order table from L2, B: |Y|^2 from LDS, both blocks share each B read)
+//   max   per-wave column max -> LDS, barrier, every wave takes the chunk max (fixed order) and the running max
+//   e     e = exp(lp - m) of the wave's own 32 components -> LDS (the filter's B layout), column sums -> LDS, barrier
+//   F     wave w: its N/4 bins over the chunk's 128 components: F[bin][obs] = alpha F + w[comp][bin] e[comp][obs]
+// Layout: the spectra tile T (16 x (N+1) complex) carries the y load and the forward FFT; the lane's filter-phase
+// spectra (bins bin0 + 16 t + hq + 4 r) move to registers and the tile is reused for |Y|^2 (in the lp B layout),
+// e and the per-wave column maxima / sums; after the last chunk it takes Z = Y f for the inverse FFT.
+template <int N>
+struct FftChunkLds {
+  static constexpr int TS = 16, RS = N + 1;
+  static constexpr size_t tile = (size_t)TS * RS * 16;
+  static constexpr size_t y2 = (size_t)N * TS * 8, e = (size_t)128 * TS * 8, sm = (size_t)2 * 4 * TS * 8;
+  static constexpr size_t body = tile > y2 + e + sm ? tile : y2 + e + sm;
+  static constexpr size_t bytes = 128 * 16 + body;
+};
+
+template <int N, int OUT>
+__global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int lg2, int Kp,
+                                                      const double2* __restrict__ y, const double* __restrict__ pr,
+                                                      const double* __restrict__ pc, const double* __restrict__ pw,
+                                                      double2* __restrict__ h, double* __restrict__ om,
+                                                      double* __restrict__ os, float* __restrict__ oa) {
+  constexpr int TS = 16, RS = N + 1, lgTS = 4;
+  constexpr int lgN = __builtin_ctz(N);
+  constexpr int NB = N / 4;    // bins per wave in the filter product
+  constexpr int NTW = NB / 16;  // the wave's 16-bin filter tiles
+  constexpr int NTF = N / 16;   // 16-bin tiles of the whole filter table
+  constexpr int NL = N / 8;     // 16-byte lp operand loads per block (two k-steps each)
+  constexpr int NWF = N / 8;    // 16-byte filter operand loads per block
+  constexpr int CB = 8;         // component blocks per chunk (two per wave)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double2* tw = reinterpret_cast<double2*>(smem);
+  double2* T = tw + 128;
+  double2* Y2 = T;                                                 // [N/8][4][16] (k-steps 2i, 2i+1 of the lp B)
+  double2* E = reinterpret_cast<double2*>(reinterpret_cast<double*>(T) + N * TS);  // [CB * 2][4][16]
+  double* SM = reinterpret_cast<double*>(E + CB * 2 * 64);         // [2][4][16] column maxima, column sums
+  const int tid = threadIdx.x;
+  const long long b0 = (long long)blockIdx.x * TS;
+  const int rows = (int)((B - b0) < TS ? (B - b0) : TS);
+  FW_STAMP_DECL
+
+  for (int t = tid; t < 128; t += 256) {
+    double sn, cs;
+    sincospi(-(double)t / 128.0, &sn, &cs);
+    tw[t] = make_double2(cs, sn);
+  }
+  {  // all loads in flight at once; rows past the batch end read a clamped (valid) row and are stored as 0
+    constexpr int NLY = TS * N / 256;
+    const double2* yt = y + b0 * N;
+    double2 v[NLY];
+#pragma unroll
+    for (int i = 0; i < NLY; ++i) {
+      const int e = tid + 256 * i, r = e >> lgN;
+      v[i] = yt[(r < rows ? r : rows - 1) * N + (e & (N - 1))];
+    }
+#pragma unroll
+    for (int i = 0; i < NLY; ++i) {
+      const int e = tid + 256 * i, r = e >> lgN;
+      T[r * RS + (e & (N - 1))] = (r < rows) ? v[i] : make_double2(0.0, 0.0);
+    }
+  }
+  __syncthreads();
+  FW_STAMP(0);
+  fft_axis_passes<false>(T, lgTS, RS, lgN, lg2, 1, tw);
+  if (lg1 > 0) fft_axis_passes<false>(T, lgTS, RS, lgN, lg1, 1 << lg2, tw);
+  FW_STAMP(1);
+
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int col = lane & 15, hq = lane >> 4;
+  const int bin0 = wid * NB;
+  // the lane's filter-phase spectra: tile t, accumulator row hq + 4 r = bin bin0 + 16 t + hq + 4 r, observation col
+  double2 yv[NTW * 4];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) yv[4 * t + r] = T[col * RS + bin0 + 16 * t + hq + 4 * r];
+  {  // |Y|^2 in the lp B layout: pair (k-step 2i, 2i + 1) of lane (hq, col) = bins 8 i + hq, 8 i + 4 + hq
+    constexpr int NP = N * TS / 2 / 256;
+    double2 q[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const int p = tid + 256 * j, s = p & 15, rest = p >> 4;
+      const int bq = 8 * (rest >> 2) + (rest & 3);
+      const double2 a = T[s * RS + bq], b = T[s * RS + bq + 4];
+      q[j] = make_double2(a.x * a.x + a.y * a.y, b.x * b.x + b.y * b.y);
+    }
+    __syncthreads();  // every spectrum value is in registers: the tile takes |Y|^2, e and the column statistics
+#pragma unroll
+    for (int j = 0; j < NP; ++j) Y2[tid + 256 * j] = q[j];  // index = (i * 4 + hq) * 16 + s
+    __syncthreads();
+  }
+  FW_STAMP(2);
+
+  f64x4 F[NTW];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t)
+    for (int r = 0; r < 4; ++r) F[t][r] = 0.0;
+  double m = -__builtin_inf(), ssum = 0.0;
+  const int ncb = Kp >> 4;
+  const double2* PR = reinterpret_cast<const double2*>(pr) + lane;
+  const double2* PW = reinterpret_cast<const double2*>(pw) + lane;
+  const double2* Y2l = Y2 + hq * 16 + col;
+  for (int c0 = 0; c0 < ncb; c0 += CB) {
+    const int cb0 = c0 + wid, cb1 = cb0 + 4;
+    const bool v0 = cb0 < ncb, v1 = cb1 < ncb;  // wave-uniform
+    f64x4 C0, C1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      C0[r] = v0 ? pc[16 * cb0 + hq + 4 * r] : -__builtin_inf();
+      C1[r] = v1 ? pc[16 * cb1 + hq + 4 * r] : -__builtin_inf();
+    }
+    if (v1) {
+      const double2* A0 = PR + (long long)cb0 * NL * 64;
+      const double2* A1 = PR + (long long)cb1 * NL * 64;
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        const double2 a0 = A0[i * 64], a1 = A1[i * 64], b = Y2l[i * 64];
+        C0 = mfma16x16x4d(a0.x, b.x, C0);
+        C1 = mfma16x16x4d(a1.x, b.x, C1);
+        C0 = mfma16x16x4d(a0.y, b.y, C0);
+        C1 = mfma16x16x4d(a1.y, b.y, C1);
+      }
+    } else if (v0) {
+      const double2* A0 = PR + (long long)cb0 * NL * 64;
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        const double2 a0 = A0[i * 64], b = Y2l[i * 64];
+        C0 = mfma16x16x4d(a0.x, b.x, C0);
+        C0 = mfma16x16x4d(a0.y, b.y, C0);
+      }
+    }
+    FW_STAMP(3);
+    // chunk maximum per observation: per-wave column maxima, then all four in a fixed order
+    const double lm = col_max4(fmax(fmax(fmax(C0[0], C0[1]), fmax(C0[2], C0[3])),
+                                    fmax(fmax(C1[0], C1[1]), fmax(C1[2], C1[3]))));
+    if (hq == 0) SM[wid * 16 + col] = lm;
+    __syncthreads();
+    const double mn = fmax(fmax(m, fmax(SM[col], SM[16 + col])), fmax(SM[32 + col], SM[48 + col]));
+    const double sh = (mn == -__builtin_inf()) ? 0.0 : mn;
+    const double alpha = exp(m - sh);
+    // e of the wave's own components, in the filter's B layout: k-step ks = 4 (local block) + r covers the
+    // components 4 ks + hq; pair (ks even, ks + 1) per 16-byte slot
+    double ls = 0.0;
+    {
+      double e[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) e[r] = v0 ? exp(C0[r] - sh) : 0.0;
+      ls += (e[0] + e[1]) + (e[2] + e[3]);
+      E[((2 * wid) * 4 + hq) * 16 + col] = make_double2(e[0], e[1]);
+      E[((2 * wid + 1) * 4 + hq) * 16 + col] = make_double2(e[2], e[3]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) e[r] = v1 ? exp(C1[r] - sh) : 0.0;
+      ls += (e[0] + e[1]) + (e[2] + e[3]);
+      E[((2 * (wid + 4)) * 4 + hq) * 16 + col] = make_double2(e[0], e[1]);
+      E[((2 * (wid + 4) + 1) * 4 + hq) * 16 + col] = make_double2(e[2], e[3]);
+    }
+    ls = col_sum4(ls);
+    if (hq == 0) SM[64 + wid * 16 + col] = ls;
+    __syncthreads();
+    ssum = ssum * alpha + ((SM[64 + col] + SM[80 + col]) + (SM[96 + col] + SM[112 + col]));
+    m = mn;
+    FW_STAMP(4);
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) F[t] *= alpha;
+    // filter over the chunk's blocks (padding blocks beyond ncb carry e = 0 and are skipped)
+    // the operands of block bl + 1 are fetched while block bl computes
+    const int nbl = (ncb - c0) < CB ? (ncb - c0) : CB;
+    constexpr int NWL = 2 * NTW;  // 16-byte filter operand loads per block and wave: (r, tile pair tp)
+    const double2* Wb = PW + (long long)c0 * NWF * 64 + ((wid * NTW) >> 1) * 64;
+    auto load_w = [&](int bl, double2 (&wv)[NWL]) {
+      const double2* W = Wb + (long long)bl * NWF * 64;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int tp = 0; tp < NTW / 2; ++tp) wv[r * (NTW / 2) + tp] = W[((r * NTF) >> 1) * 64 + tp * 64];
+    };
+    double2 wn[NWL];
+    load_w(0, wn);
+    for (int bl = 0; bl < nbl; ++bl) {
+      double2 wc[NWL];
+#pragma unroll
+      for (int i = 0; i < NWL; ++i) wc[i] = wn[i];
+      if (bl + 1 < nbl) load_w(bl + 1, wn);
+#pragma unroll
+      for (int rp = 0; rp < 2; ++rp) {
+        const double2 ev = E[((2 * bl + rp) * 4 + hq) * 16 + col];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+          const int r = 2 * rp + rr;
+          const double eb = rr ? ev.y : ev.x;
+#pragma unroll
+          for (int tp = 0; tp < NTW / 2; ++tp) {  // filter table pair (j, j + 1), j = r NTF + t: tiles t, t + 1
+            const double2 wv = wc[r * (NTW / 2) + tp];
+            F[2 * tp] = mfma16x16x4d(wv.x, eb, F[2 * tp]);
+            F[2 * tp + 1] = mfma16x16x4d(wv.y, eb, F[2 * tp + 1]);
+          }
+        }
+      }
+    }
+    FW_STAMP(5);
+  }
+  __syncthreads();  // every wave is done with |Y|^2 and e: the tile takes Z
+  const double sc = (OUT == 0) ? 1.0 / ssum : 1.0;
+#pragma unroll
+  for (int t = 0; t < NTW; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double2 v = yv[4 * t + r];
+      const double f = F[t][r] * sc;
+      T[col * RS + bin0 + 16 * t + hq + 4 * r] = make_double2(v.x * f, v.y * f);
+    }
+  if ((OUT == 3 || OUT == 4) && wid == 0 && hq == 0 && col < rows) {
+    om[b0 + col] = m;
+    os[b0 + col] = ssum;
+  }
+  __syncthreads();
+  if (lg1 > 0) fft_axis_passes<true>(T, lgTS, RS, lgN, lg1, 1 << lg2, tw);
+  fft_axis_passes<true>(T, lgTS, RS, lgN, lg2, 1, tw);
+  FW_STAMP(6);
+  if (OUT == 3) {
+    float2* at = reinterpret_cast<float2*>(oa) + b0 * N;
+#pragma unroll 4
+    for (int e = tid; e < rows * N; e += 256) {
+      const double2 v = T[(e >> lgN) * RS + (e & (N - 1))];
+      at[e] = make_float2((float)v.x, (float)v.y);
+    }
+  } else if (OUT == 4) {
+    double2* at = reinterpret_cast<double2*>(oa) + b0 * N;
+#pragma unroll 4
+    for (int e = tid; e < rows * N; e += 256) at[e] = T[(e >> lgN) * RS + (e & (N - 1))];
+  } else if (rows == TS) {
+    double2* ht = h + b0 * N;
+    constexpr int NLY = TS * N / 256;
+    double2 v[NLY];
+#pragma unroll
+    for (int i = 0; i < NLY; ++i) {
+      const int e = tid + 256 * i;
+      v[i] = T[(e >> lgN) * RS + (e & (N - 1))];
+    }
+#pragma unroll
+    for (int i = 0; i < NLY; ++i) ht[tid + 256 * i] = v[i];
+  } else {
+    double2* ht = h + b0 * N;
+#pragma unroll 4
+    for (int e = tid; e < rows * N; e += 256) ht[e] = T[(e >> lgN) * RS + (e & (N - 1))];
+  }
+  FW_STAMP(7);
+  FW_STAMP_FLUSH
+}
+
 // natural-order per-bin tables of k_fft_prep -> the kernel's storage order (bit-reversed per axis),
 // negated rinv, components padded to Kp (padding: c' = -inf, zero tables); N <= 64: fragment order of
 // k_fft_wave, otherwise the row-major N x Kp / Kp x N order of k_fft_mfma
-__global__ __launch_bounds__(256) void k_fft_pack(int N, int lg1, int lg2, int K, int Kp, int has_mean,
+__global__ __launch_bounds__(256) void k_fft_pack(int N, int lg1, int lg2, int K, int Kp, int has_mean, int frag,
                                                   const double* __restrict__ rinvT, const double2* __restrict__ uT,
                                                   const double* __restrict__ cprime, const double* __restrict__ wT,
                                                   const double2* __restrict__ bT, double* __restrict__ pr,
@@ -767,7 +1021,7 @@ __global__ __launch_bounds__(256) void k_fft_pack(int N, int lg1, int lg2, int K
   const int n2m = (1 << lg2) - 1;
   auto bin_of = [&](int p) { return (brev(p >> lg2, lg1) << lg2) | brev(p & n2m, lg2); };
   const long long total = (long long)N * Kp;
-  if (N <= 64) {  // fragment order: e = ((cb Q + i) 64 + lane) 2 + s, Q = N / 8 16-byte loads per block and table
+  if (N <= 64 || (!has_mean && frag)) {  // fragment order: e = ((cb Q + i) 64 + lane) 2 + s, Q = N / 8 16-byte loads per block and table
     const int Q = N / 8, NT = N / 16;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
          e += (long long)gridDim.x * blockDim.x) {
@@ -876,14 +1130,31 @@ hipError_t launch_wave_t(const QceFftEstArgs& a, hipStream_t st) {
 }
 
 
+template <int N, int OUT>
+hipError_t launch_chunk_t(const QceFftEstArgs& a, hipStream_t st) {
+  constexpr size_t lds = FftChunkLds<N>::bytes;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_fft_chunk<N, OUT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int lg1 = __builtin_ctz(a.n1), lg2 = __builtin_ctz(a.n2);
+  dim3 grid((unsigned)((a.B + 15) / 16));
+  hipLaunchKernelGGL((k_fft_chunk<N, OUT>), grid, dim3(256), lds, st, a.B, lg1, lg2, a.Kp, a.y, a.pr, a.pc, a.pw,
+                     a.h, a.om, a.os, a.oa);
+  return hipGetLastError();
+}
+
 template <int OUT, bool HM>
 hipError_t launch_mfma_out(const QceFftEstArgs& a, hipStream_t st) {
   switch (a.N) {
     case 16: return launch_wave_t<16, OUT, HM>(a, st);
     case 32: return launch_wave_t<32, OUT, HM>(a, st);
     case 64: return launch_wave_t<64, OUT, HM>(a, st);
-    case 128: return launch_mfma_t<128, OUT, HM>(a, st);
-    case 256: return launch_mfma_t<256, OUT, HM>(a, st);
+    case 128: return (!HM && a.chunk) ? launch_chunk_t<128, OUT>(a, st) : launch_mfma_t<128, OUT, HM>(a, st);
+    case 256: return (!HM && a.chunk) ? launch_chunk_t<256, OUT>(a, st) : launch_mfma_t<256, OUT, HM>(a, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -899,7 +1170,8 @@ hipError_t qce_launch_fft_pack(const QceFftEstArgs& a, const double* rinvT, cons
   const int lg1 = __builtin_ctz(a.n1), lg2 = __builtin_ctz(a.n2);
   const long long total = (long long)a.N * a.Kp;
   const int blocks = (int)((total + 255) / 256);
-  hipLaunchKernelGGL(k_fft_pack, dim3(blocks), dim3(256), 0, st, a.N, lg1, lg2, a.K, a.Kp, a.has_mean, rinvT, uT,
+  hipLaunchKernelGGL(k_fft_pack, dim3(blocks), dim3(256), 0, st, a.N, lg1, lg2, a.K, a.Kp, a.has_mean,
+                     a.chunk, rinvT, uT,
                      cprime, wT, bT, const_cast<double*>(a.pr), const_cast<double*>(a.pur),
                      const_cast<double*>(a.pui), const_cast<double*>(a.pc), const_cast<double*>(a.pw),
                      const_cast<double*>(a.pbr), const_cast<double*>(a.pbi));

@@ -196,7 +196,8 @@ struct QceFftEstArgs {
   // MFMA kernel tables (qce_fft_mfma.hip, storage order, components padded to Kp)
   int Kp;
   const double *pr, *pur, *pui, *pc, *pw, *pbr, *pbi;
-  int cu;  // compute units of the device (persistent grid of k_fft_wave)
+  int cu;     // compute units of the device (persistent grid of k_fft_wave)
+  int chunk;  // zero-mean N = 128, 256: k_fft_chunk on fragment-order tables (else k_fft_mfma, row-major)
 };
 bool qce_fft_pow2(int v);
 int qce_fft_tile(int N, int K);  // 0: no tile fits (K too large)

@@ -444,6 +444,47 @@ def test_fourier_mfma_kernel_vs_lds_kernel(K, N, blocks, B, n_bits, mean, monkey
         assert rel_fro(out[kern][2], ho) < tol, kern
 
 
+@pytest.mark.parametrize("K,N,blocks,B,n_bits", [
+    (128, 256, (4, 64), 1003, 2),   # cfg5 geometry: one chunk of 8 blocks, two per wave
+    (200, 256, (16, 16), 517, 3),   # K = 200 -> 13 blocks: a second chunk of 5 (waves 1-3 one block each)
+    (256, 128, (8, 16), 301, 2),    # two whole chunks (the Fourier path's largest K)
+    (130, 128, None, 250, 2),       # 9 blocks: a second chunk of one block
+    (7, 128, (2, 64), 33, 1),       # one padded block, three idle waves
+])
+def test_fourier_chunk_kernel(K, N, blocks, B, n_bits, monkeypatch):
+    """k_fft_chunk (zero-mean N = 128, 256: components split over the waves for lp / softmax, bins for the
+    filter, two barriers per 128-component chunk) against the FP64 oracle and the bin-split k_fft_mfma
+    (QCE_FFT_CHUNK=0), 'all' mode and both K-shard partial accumulators."""
+    _gpu_or_skip()
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import _lib, inputs
+    from quantized_channel_estimation_amd.sharding import combine_partials_numpy
+    cov = "circulant" if blocks is None else "block-circulant"
+    means, covs, w = inputs.synthetic_model(K, N, cov_type=cov, seed=K + 1, blocks=blocks)
+    means = np.zeros_like(means)
+    rng = np.random.default_rng(K * N)
+    h, _ = inputs.scm_generate(B, 1, N, rng, n_path=3)
+    qz = (None, None, None)
+    if n_bits != 1:
+        qz = inputs.get_quantizer([5.0], n_bits, "uniform")[5.0]
+    y = inputs.get_observation_nbit(h[:, 0, :].astype(complex), 5.0, None, n_bits, qz[0], qz[1], rng=rng)
+    out = {}
+    for chunk in ("1", "0"):
+        monkeypatch.setenv("QCE_FFT_CHUNK", chunk)
+        dm = _lib.DeviceModel(means, covs, w)
+        dm.prepare(None, 5.0, float(n_bits))
+        assert dm.structure()[2] == 1
+        out[chunk] = (dm.estimate(y), combine_partials_numpy([dm.partial(y)], N),
+                      combine_partials_numpy([dm.partial64(y)], N))
+        dm.close()
+    ho = O.estimate(means, covs, w, y, 5.0, N, None, "all", n_bits, "uniform", qz)
+    tol = 1e-9 if n_bits != 1 else 1e-7
+    assert rel_fro(out["1"][0], ho) < tol, rel_fro(out["1"][0], ho)
+    assert rel_fro(out["1"][0], out["0"][0]) < 1e-12
+    assert rel_fro(out["1"][1], ho) < 1e-6  # qce_estimate_partial's acc is fp32 by its ABI
+    assert rel_fro(out["1"][2], ho) < tol
+
+
 @pytest.mark.parametrize("K,N,blocks,B,n_bits,qtype,mean", [
     (128, 64, None, 70013, 3, "lloyd", False),   # cfg3 geometry: two whole rounds of tiles + a ragged tail
     (64, 64, (8, 8), 70013, 1, "uniform", False),  # 2-D transform through the same phases
