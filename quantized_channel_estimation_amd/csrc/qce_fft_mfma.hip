@@ -753,6 +753,113 @@ __global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wave(long long B, long 
   FW_STAMP_FLUSH
 }
 
+// ---- register-resident transform of 16 points per thread (N = 256 in two passes of four radix-2 stages) ----
+// v * e^{-2 pi i mm / 16} (INV: e^{+...}), mm < 8 compile-time after unrolling
+template <bool INV>
+QCE_DEV double2 rootmul16(double2 v, int mm) {
+  if (!(mm & 1)) return rootmul<INV>(v, 8, mm >> 1);
+  constexpr double C1 = 0.92387953251128675613, S1 = 0.38268343236508977173;  // cos, sin (pi / 8)
+  const double c = (mm == 1) ? C1 : (mm == 3) ? S1 : (mm == 5) ? -S1 : -C1;
+  const double s = (mm == 1) ? S1 : (mm == 3) ? C1 : (mm == 5) ? C1 : S1;  // sin(2 pi mm / 16)
+  return INV ? make_double2(v.x * c - v.y * s, v.x * s + v.y * c) : make_double2(v.x * c + v.y * s, v.y * c - v.x * s);
+}
+template <bool INV>
+QCE_DEV double2 root_any(double2 v, int P, int mm) {
+  return P == 16 ? rootmul16<INV>(v, mm) : rootmul<INV>(v, P, mm);
+}
+
+// Radix-2^RL group on the registers x[S m], m < 2^RL: the stages of one contiguous bit range of one axis, first
+// half-distance 2^lgD (axis units), j = the axis position bits below the range (the group twiddle W_{2D_s}^j;
+// JZ: j == 0 for every thread).  Forward: DIF stages, inverse: the same stages reversed (DIT), conjugate twiddles --
+// the arithmetic of fft_pass with all R elements in one thread.
+template <int RL, bool INV, int S, bool JZ>
+QCE_DEV void reg_group(double2* x, int lgD, int j, const double2* tw) {
+  constexpr int R = 1 << RL;
+  double2 w[RL];
+  if constexpr (!JZ) {
+#pragma unroll
+    for (int sI = 0; sI < RL; ++sI) {
+      w[sI] = tw[j << (7 - (lgD - sI))];
+      if (INV) w[sI].y = -w[sI].y;
+    }
+  }
+  if constexpr (!INV) {
+#pragma unroll
+    for (int sI = 0; sI < RL; ++sI) {
+      const int half = R >> (sI + 1);
+#pragma unroll
+      for (int m = 0; m < R; ++m) {
+        if (m & half) continue;
+        const double2 a = x[S * m], b = x[S * (m + half)];
+        x[S * m] = cadd(a, b);
+        double2 d = csub(a, b);
+        if constexpr (!JZ) d = cmul(d, w[sI]);
+        x[S * (m + half)] = root_any<false>(d, 2 * half, m & (half - 1));
+      }
+    }
+  } else {
+#pragma unroll
+    for (int sI = RL - 1; sI >= 0; --sI) {
+      const int half = R >> (sI + 1);
+#pragma unroll
+      for (int m = 0; m < R; ++m) {
+        if (m & half) continue;
+        const double2 a = x[S * m];
+        double2 b = x[S * (m + half)];
+        if constexpr (!JZ) b = cmul(b, w[sI]);
+        b = root_any<true>(b, 2 * half, m & (half - 1));
+        x[S * m] = cadd(a, b);
+        x[S * (m + half)] = csub(a, b);
+      }
+    }
+  }
+}
+
+// One pass over a thread's 16 points (array index = 4 bits of the storage position): array bits [0, RA) are axis n2
+// (segment A), [RA, 4) axis n1 (segment B).  The axes are independent, so the segments run in either order.
+template <int RA, bool INV, bool JZA, bool JZB>
+QCE_DEV void reg_pass16(double2 (&x)[16], int lgDA, int jA, int lgDB, int jB, const double2* tw) {
+  constexpr int RB = 4 - RA;
+  if constexpr (RB > 0) {
+#pragma unroll
+    for (int a = 0; a < (1 << RA); ++a) reg_group<RB, INV, (1 << RA), JZB>(x + a, lgDB, jB, tw);
+  }
+  if constexpr (RA > 0) {
+#pragma unroll
+    for (int b = 0; b < (1 << RB); ++b) reg_group<RA, INV, 1, JZA>(x + (b << RA), lgDA, jA, tw);
+  }
+}
+
+// N = 256 = n1 n2 (lg2 = log2 n2): the forward transform's stages in descending storage bit order are bits 7..4
+// (pass 1) and 3..0 (pass 2) -- per axis high bits before low bits, as DIF requires.  Pass 1: the thread's points
+// share the storage bits 0-3 (g), pass 2 the bits 4-7.
+template <bool INV>
+QCE_DEV void fft256_pass1(double2 (&x)[16], int lg2, int g, const double2* tw) {
+  switch (lg2) {  // segment A = n2 bits [4, lg2), B = n1 bits [max(lg2, 4), 8)
+    case 8: reg_pass16<4, INV, false, true>(x, 7, g, 0, 0, tw); break;
+    case 7: reg_pass16<3, INV, false, true>(x, 6, g, 0, 0, tw); break;
+    case 6: reg_pass16<2, INV, false, true>(x, 5, g, 1, 0, tw); break;
+    case 5: reg_pass16<1, INV, false, true>(x, 4, g, 2, 0, tw); break;
+    case 4: reg_pass16<0, INV, true, true>(x, 0, 0, 3, 0, tw); break;
+    default: reg_pass16<0, INV, true, false>(x, 0, 0, 7 - lg2, g >> lg2, tw); break;  // n1 bits 4-7, j = n1 bits < 4
+  }
+}
+template <bool INV>
+QCE_DEV void fft256_pass2(double2 (&x)[16], int lg2, const double2* tw) {
+  switch (lg2 >= 4 ? 4 : lg2) {  // segment A = n2 bits [0, min(lg2, 4)), B = n1 bits [lg2, 4)
+    case 4: reg_pass16<4, INV, true, true>(x, 3, 0, 0, 0, tw); break;
+    case 3: reg_pass16<3, INV, true, true>(x, 2, 0, 0, 0, tw); break;
+    case 2: reg_pass16<2, INV, true, true>(x, 1, 0, 1, 0, tw); break;
+    case 1: reg_pass16<1, INV, true, true>(x, 0, 0, 2, 0, tw); break;
+    default: reg_pass16<0, INV, true, true>(x, 0, 0, 3, 0, tw); break;
+  }
+}
+
+// Filter-phase bin of k_fft_chunk<256>: wave w = t / 4 owns the storage positions with bits 4-7 = hq + 4 w, its tile
+// t % 4 and accumulator register r (row hq + 4 r) give bits 0-3 = r + 4 (t % 4) -- exactly the 16 points a lane
+// holds after pass 2, so the spectra and Z never pass through LDS between the transforms and the filter.
+QCE_DEV int chunk256_bin(int t, int row) { return (((row & 3) + 4 * (t >> 2)) << 4) | ((row >> 2) + 4 * (t & 3)); }
+
 // Zero-mean models, N = 128, 256: one workgroup (4 waves) per 16 observations, the components split over the waves
 // for the log-probabilities and the bins split over the waves for the filter, so the softmax of every (component,
 // observation) is evaluated exactly once and the waves meet at two barriers per chunk of 128 components (not per
@@ -799,55 +906,98 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
   const int rows = (int)((B - b0) < TS ? (B - b0) : TS);
   FW_STAMP_DECL
 
-  for (int t = tid; t < 128; t += 256) {
-    double sn, cs;
-    sincospi(-(double)t / 128.0, &sn, &cs);
-    tw[t] = make_double2(cs, sn);
-  }
-  {  // all loads in flight at once; rows past the batch end read a clamped (valid) row and are stored as 0
-    constexpr int NLY = TS * N / 256;
-    const double2* yt = y + b0 * N;
-    double2 v[NLY];
-#pragma unroll
-    for (int i = 0; i < NLY; ++i) {
-      const int e = tid + 256 * i, r = e >> lgN;
-      v[i] = yt[(r < rows ? r : rows - 1) * N + (e & (N - 1))];
-    }
-#pragma unroll
-    for (int i = 0; i < NLY; ++i) {
-      const int e = tid + 256 * i, r = e >> lgN;
-      T[r * RS + (e & (N - 1))] = (r < rows) ? v[i] : make_double2(0.0, 0.0);
-    }
-  }
-  __syncthreads();
-  FW_STAMP(0);
-  fft_axis_passes<false>(T, lgTS, RS, lgN, lg2, 1, tw);
-  if (lg1 > 0) fft_axis_passes<false>(T, lgTS, RS, lgN, lg1, 1 << lg2, tw);
-  FW_STAMP(1);
-
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int col = lane & 15, hq = lane >> 4;
   const int bin0 = wid * NB;
-  // the lane's filter-phase spectra: tile t, accumulator row hq + 4 r = bin bin0 + 16 t + hq + 4 r, observation col
-  double2 yv[NTW * 4];
+  double2 yv[NTW * 4];  // the lane's filter-phase spectra (tile t, accumulator row hq + 4 r: yv[4 t + r])
+  if constexpr (N == 256) {
+    // pass 1 straight from HBM: thread (s = tid / 16, g = tid % 16) holds positions g + 16 i of observation s (each
+    // i a 256-byte contiguous run over 16 lanes); pass 2 thread (wave w, hq, col) the positions 16 (hq + 4 w) + i of
+    // observation col, which stay in registers as yv
+    const int s1 = tid >> 4, g = tid & 15;
+    {
+      const double2* yr = y + (b0 + (s1 < rows ? s1 : rows - 1)) * N + g;
+      double2 x[16];
 #pragma unroll
-  for (int t = 0; t < NTW; ++t)
+      for (int i = 0; i < 16; ++i) x[i] = yr[16 * i];
+      for (int t = tid; t < 128; t += 256) {
+        double sn, cs;
+        sincospi(-(double)t / 128.0, &sn, &cs);
+        tw[t] = make_double2(cs, sn);
+      }
+      __syncthreads();
+      FW_STAMP(0);
+      if (s1 >= rows) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) yv[4 * t + r] = T[col * RS + bin0 + 16 * t + hq + 4 * r];
-  {  // |Y|^2 in the lp B layout: pair (k-step 2i, 2i + 1) of lane (hq, col) = bins 8 i + hq, 8 i + 4 + hq
-    constexpr int NP = N * TS / 2 / 256;
-    double2 q[NP];
+        for (int i = 0; i < 16; ++i) x[i] = make_double2(0.0, 0.0);
+      }
+      fft256_pass1<false>(x, lg2, g, tw);
 #pragma unroll
-    for (int j = 0; j < NP; ++j) {
-      const int p = tid + 256 * j, s = p & 15, rest = p >> 4;
-      const int bq = 8 * (rest >> 2) + (rest & 3);
-      const double2 a = T[s * RS + bq], b = T[s * RS + bq + 4];
-      q[j] = make_double2(a.x * a.x + a.y * a.y, b.x * b.x + b.y * b.y);
+      for (int i = 0; i < 16; ++i) T[s1 * RS + g + 16 * i] = x[i];
     }
-    __syncthreads();  // every spectrum value is in registers: the tile takes |Y|^2, e and the column statistics
-#pragma unroll
-    for (int j = 0; j < NP; ++j) Y2[tid + 256 * j] = q[j];  // index = (i * 4 + hq) * 16 + s
     __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 16; ++i) yv[i] = T[col * RS + 16 * (hq + 4 * wid) + i];
+    fft256_pass2<false>(yv, lg2, tw);
+    FW_STAMP(1);
+    __syncthreads();  // every spectrum value is in registers: the tile takes |Y|^2, e and the column statistics
+    // |Y|^2 in the lp B layout (k-step u = p / 4 covers p = 4 u + hq'): position 16 (hq + 4 w) + r + 4 t is k-step
+    // u = 4 (hq + 4 w) + t, row hq' = r; the pair (t even, t odd) is one 16-byte slot
+#pragma unroll
+    for (int tp = 0; tp < 2; ++tp)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double2 a = yv[r + 8 * tp], b = yv[r + 8 * tp + 4];
+        Y2[((2 * (hq + 4 * wid) + tp) * 4 + r) * 16 + col] =
+            make_double2(a.x * a.x + a.y * a.y, b.x * b.x + b.y * b.y);
+      }
+    __syncthreads();
+  } else {
+    for (int t = tid; t < 128; t += 256) {
+      double sn, cs;
+      sincospi(-(double)t / 128.0, &sn, &cs);
+      tw[t] = make_double2(cs, sn);
+    }
+    {  // all loads in flight at once; rows past the batch end read a clamped (valid) row and are stored as 0
+      constexpr int NLY = TS * N / 256;
+      const double2* yt = y + b0 * N;
+      double2 v[NLY];
+#pragma unroll
+      for (int i = 0; i < NLY; ++i) {
+        const int e = tid + 256 * i, r = e >> lgN;
+        v[i] = yt[(r < rows ? r : rows - 1) * N + (e & (N - 1))];
+      }
+#pragma unroll
+      for (int i = 0; i < NLY; ++i) {
+        const int e = tid + 256 * i, r = e >> lgN;
+        T[r * RS + (e & (N - 1))] = (r < rows) ? v[i] : make_double2(0.0, 0.0);
+      }
+    }
+    __syncthreads();
+    FW_STAMP(0);
+    fft_axis_passes<false>(T, lgTS, RS, lgN, lg2, 1, tw);
+    if (lg1 > 0) fft_axis_passes<false>(T, lgTS, RS, lgN, lg1, 1 << lg2, tw);
+    FW_STAMP(1);
+    // bin bin0 + 16 t + hq + 4 r, observation col
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) yv[4 * t + r] = T[col * RS + bin0 + 16 * t + hq + 4 * r];
+    {  // |Y|^2 in the lp B layout: pair (k-step 2i, 2i + 1) of lane (hq, col) = bins 8 i + hq, 8 i + 4 + hq
+      constexpr int NP = N * TS / 2 / 256;
+      double2 q[NP];
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        const int p = tid + 256 * j, s = p & 15, rest = p >> 4;
+        const int bq = 8 * (rest >> 2) + (rest & 3);
+        const double2 a = T[s * RS + bq], b = T[s * RS + bq + 4];
+        q[j] = make_double2(a.x * a.x + a.y * a.y, b.x * b.x + b.y * b.y);
+      }
+      __syncthreads();  // every spectrum value is in registers: the tile takes |Y|^2, e and the column statistics
+#pragma unroll
+      for (int j = 0; j < NP; ++j) Y2[tid + 256 * j] = q[j];  // index = (i * 4 + hq) * 16 + s
+      __syncthreads();
+    }
   }
   FW_STAMP(2);
 
@@ -961,48 +1111,83 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
   }
   __syncthreads();  // every wave is done with |Y|^2 and e: the tile takes Z
   const double sc = (OUT == 0) ? 1.0 / ssum : 1.0;
-#pragma unroll
-  for (int t = 0; t < NTW; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const double2 v = yv[4 * t + r];
-      const double f = F[t][r] * sc;
-      T[col * RS + bin0 + 16 * t + hq + 4 * r] = make_double2(v.x * f, v.y * f);
-    }
   if ((OUT == 3 || OUT == 4) && wid == 0 && hq == 0 && col < rows) {
     om[b0 + col] = m;
     os[b0 + col] = ssum;
   }
-  __syncthreads();
-  if (lg1 > 0) fft_axis_passes<true>(T, lgTS, RS, lgN, lg1, 1 << lg2, tw);
-  fft_axis_passes<true>(T, lgTS, RS, lgN, lg2, 1, tw);
-  FW_STAMP(6);
-  if (OUT == 3) {
-    float2* at = reinterpret_cast<float2*>(oa) + b0 * N;
-#pragma unroll 4
-    for (int e = tid; e < rows * N; e += 256) {
-      const double2 v = T[(e >> lgN) * RS + (e & (N - 1))];
-      at[e] = make_float2((float)v.x, (float)v.y);
-    }
-  } else if (OUT == 4) {
-    double2* at = reinterpret_cast<double2*>(oa) + b0 * N;
-#pragma unroll 4
-    for (int e = tid; e < rows * N; e += 256) at[e] = T[(e >> lgN) * RS + (e & (N - 1))];
-  } else if (rows == TS) {
-    double2* ht = h + b0 * N;
-    constexpr int NLY = TS * N / 256;
-    double2 v[NLY];
+  if constexpr (N == 256) {  // inverse pass 2 on the registers, one LDS exchange, inverse pass 1, store from registers
 #pragma unroll
-    for (int i = 0; i < NLY; ++i) {
-      const int e = tid + 256 * i;
-      v[i] = T[(e >> lgN) * RS + (e & (N - 1))];
-    }
+    for (int t = 0; t < NTW; ++t)
 #pragma unroll
-    for (int i = 0; i < NLY; ++i) ht[tid + 256 * i] = v[i];
+      for (int r = 0; r < 4; ++r) {
+        const double f = F[t][r] * sc;
+        yv[4 * t + r] = make_double2(yv[4 * t + r].x * f, yv[4 * t + r].y * f);
+      }
+    fft256_pass2<true>(yv, lg2, tw);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) T[col * RS + 16 * (hq + 4 * wid) + i] = yv[i];
+    __syncthreads();
+    const int s1 = tid >> 4, g = tid & 15;
+    double2 x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = T[s1 * RS + g + 16 * i];
+    fft256_pass1<true>(x, lg2, g, tw);
+    FW_STAMP(6);
+    if (s1 < rows) {
+      const long long o = (b0 + s1) * N + g;
+      if (OUT == 3) {
+        float2* at = reinterpret_cast<float2*>(oa) + o;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) at[16 * i] = make_float2((float)x[i].x, (float)x[i].y);
+      } else if (OUT == 4) {
+        double2* at = reinterpret_cast<double2*>(oa) + o;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) at[16 * i] = x[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) h[o + 16 * i] = x[i];
+      }
+    }
   } else {
-    double2* ht = h + b0 * N;
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double2 v = yv[4 * t + r];
+        const double f = F[t][r] * sc;
+        T[col * RS + bin0 + 16 * t + hq + 4 * r] = make_double2(v.x * f, v.y * f);
+      }
+    __syncthreads();
+    if (lg1 > 0) fft_axis_passes<true>(T, lgTS, RS, lgN, lg1, 1 << lg2, tw);
+    fft_axis_passes<true>(T, lgTS, RS, lgN, lg2, 1, tw);
+    FW_STAMP(6);
+    if (OUT == 3) {
+      float2* at = reinterpret_cast<float2*>(oa) + b0 * N;
 #pragma unroll 4
-    for (int e = tid; e < rows * N; e += 256) ht[e] = T[(e >> lgN) * RS + (e & (N - 1))];
+      for (int e = tid; e < rows * N; e += 256) {
+        const double2 v = T[(e >> lgN) * RS + (e & (N - 1))];
+        at[e] = make_float2((float)v.x, (float)v.y);
+      }
+    } else if (OUT == 4) {
+      double2* at = reinterpret_cast<double2*>(oa) + b0 * N;
+#pragma unroll 4
+      for (int e = tid; e < rows * N; e += 256) at[e] = T[(e >> lgN) * RS + (e & (N - 1))];
+    } else if (rows == TS) {
+      double2* ht = h + b0 * N;
+      constexpr int NLY = TS * N / 256;
+      double2 v[NLY];
+#pragma unroll
+      for (int i = 0; i < NLY; ++i) {
+        const int e = tid + 256 * i;
+        v[i] = T[(e >> lgN) * RS + (e & (N - 1))];
+      }
+#pragma unroll
+      for (int i = 0; i < NLY; ++i) ht[tid + 256 * i] = v[i];
+    } else {
+      double2* ht = h + b0 * N;
+#pragma unroll 4
+      for (int e = tid; e < rows * N; e += 256) ht[e] = T[(e >> lgN) * RS + (e & (N - 1))];
+    }
   }
   FW_STAMP(7);
   FW_STAMP_FLUSH
@@ -1041,7 +1226,8 @@ __global__ __launch_bounds__(256) void k_fft_pack(int N, int lg1, int lg2, int K
       }
       {  // filter: r = j / NT, t = j % NT; comp 16cb + lane/16 + 4r, bin 16t + lane%16
         const int r = j / NT, t = j % NT;
-        const int k = 16 * cb + (lane >> 4) + 4 * r, p = 16 * t + (lane & 15);
+        const int k = 16 * cb + (lane >> 4) + 4 * r;
+        const int p = (N == 256) ? chunk256_bin(t, lane & 15) : 16 * t + (lane & 15);
         const bool ok = k < K;
         const long long src = (long long)k * N + bin_of(p);
         pw[e] = ok ? wT[src] : 0.0;

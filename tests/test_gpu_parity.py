@@ -450,6 +450,9 @@ def test_fourier_mfma_kernel_vs_lds_kernel(K, N, blocks, B, n_bits, mean, monkey
     (256, 128, (8, 16), 301, 2),    # two whole chunks (the Fourier path's largest K)
     (130, 128, None, 250, 2),       # 9 blocks: a second chunk of one block
     (7, 128, (2, 64), 33, 1),       # one padded block, three idle waves
+    (64, 256, None, 100, 2),        # circulant 256: both register passes on one axis
+    (40, 256, (2, 128), 90, 3),     # pass 1 = 3 bits of n2 + the n1 bit
+    (48, 256, (64, 4), 77, 2),      # n2 = 4: pass 2 = both n2 bits + 2 low n1 bits, pass 1 n1 only (j != 0)
 ])
 def test_fourier_chunk_kernel(K, N, blocks, B, n_bits, monkeypatch):
     """k_fft_chunk (zero-mean N = 128, 256: components split over the waves for lp / softmax, bins for the
