@@ -753,6 +753,52 @@ __global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wave(long long B, long 
   FW_STAMP_FLUSH
 }
 
+// Buffer-resource memory access: a wave-uniform descriptor (base, byte extent) in scalar registers plus a 32-bit
+// per-lane offset, so no 64-bit per-lane addresses occupy vector registers; loads past the extent return 0 and
+// stores past it are dropped (the ragged last tile needs no guards).
+typedef unsigned int qce_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int qce_u32x2 __attribute__((ext_vector_type(2)));
+QCE_DEV __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, (int)bytes, 0x00020000);
+}
+QCE_DEV double2 buf_ld2(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(double2, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+}
+QCE_DEV double buf_ld1(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+}
+QCE_DEV void buf_st2(double2 v, __amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(qce_u32x4, v), r, voff, soff, 0);
+}
+QCE_DEV void buf_st1f2(float2 v, __amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(qce_u32x2, v), r, voff, soff, 0);
+}
+
+// e^x for x <= 700 (x = -inf and x < -708 give 0, a weight below 1e-307 of the largest): 2^(k/32) from a 32-entry LDS
+// table (exp2_tab, 2^(j/32)) times the degree-6 Taylor polynomial of e^r, |r| <= ln2/64 (truncation 4e-18), 2^(k>>5)
+// added to the exponent field: 18 VALU against ~32 for the libm exp, about 2 ulp.
+QCE_DEV double exp_nonpos(double x, const double* __restrict__ tab) {
+  constexpr double L32 = 46.166241308446828384;      // 32 / ln 2
+  constexpr double LH = 2.1660849390173098072e-02;   // ln 2 / 32, leading bits
+  constexpr double LL = 2.3251928468788740148e-12;   // ln 2 / 32 - LH
+  const double kf = __builtin_rint(x * L32);
+  double r = fma(kf, -LH, x);
+  r = fma(kf, -LL, r);
+  const int k = (int)kf;
+  double p = fma(r, 1.0 / 720.0, 1.0 / 120.0);
+  p = fma(p, r, 1.0 / 24.0);
+  p = fma(p, r, 1.0 / 6.0);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  const double v = tab[k & 31] * p;
+  const double res = __hiloint2double(__double2hiint(v) + ((k >> 5) << 20), __double2loint(v));
+  return (x < -708.0) ? 0.0 : res;
+}
+QCE_DEV void exp2_tab_init(double* tab, int tid) {
+  if (tid < 32) tab[tid] = exp2((double)tid / 32.0);
+}
+
 // ---- register-resident transform of 16 points per thread (N = 256 in two passes of four radix-2 stages) ----
 // v * e^{-2 pi i mm / 16} (INV: e^{+...}), mm < 8 compile-time after unrolling
 template <bool INV>
@@ -815,11 +861,11 @@ QCE_DEV void reg_group(double2* x, int lgD, int j, const double2* tw) {
   }
 }
 
-// One pass over a thread's 16 points (array index = 4 bits of the storage position): array bits [0, RA) are axis n2
-// (segment A), [RA, 4) axis n1 (segment B).  The axes are independent, so the segments run in either order.
-template <int RA, bool INV, bool JZA, bool JZB>
-QCE_DEV void reg_pass16(double2 (&x)[16], int lgDA, int jA, int lgDB, int jB, const double2* tw) {
-  constexpr int RB = 4 - RA;
+// One pass over a thread's 2^RT points (array index = RT bits of the storage position): array bits [0, RA) are
+// axis n2 (segment A), [RA, RT) axis n1 (segment B).  The axes are independent, so the segments run in either order.
+template <int RT, int RA, bool INV, bool JZA, bool JZB>
+QCE_DEV void reg_pass(double2* x, int lgDA, int jA, int lgDB, int jB, const double2* tw) {
+  constexpr int RB = RT - RA;
   if constexpr (RB > 0) {
 #pragma unroll
     for (int a = 0; a < (1 << RA); ++a) reg_group<RB, INV, (1 << RA), JZB>(x + a, lgDB, jB, tw);
@@ -827,6 +873,22 @@ QCE_DEV void reg_pass16(double2 (&x)[16], int lgDA, int jA, int lgDB, int jB, co
   if constexpr (RA > 0) {
 #pragma unroll
     for (int b = 0; b < (1 << RB); ++b) reg_group<RA, INV, 1, JZA>(x + (b << RA), lgDA, jA, tw);
+  }
+}
+template <int RA, bool INV, bool JZA, bool JZB>
+QCE_DEV void reg_pass16(double2 (&x)[16], int lgDA, int jA, int lgDB, int jB, const double2* tw) {
+  reg_pass<4, RA, INV, JZA, JZB>(x, lgDA, jA, lgDB, jB, tw);
+}
+
+// N = 64 = n1 n2: pass 1 = storage bits 5, 4 on a group of 4 points sharing the bits 0-3 (g); segment A = n2 bits
+// [4, min(lg2, 6)), B = n1 bits [max(lg2, 4), 6), j = the axis bits below the segment
+template <bool INV>
+QCE_DEV void fft64_pass1(double2* x, int lg2, int g, const double2* tw) {
+  switch (lg2) {
+    case 6: reg_pass<2, 2, INV, false, true>(x, 5, g, 0, 0, tw); break;
+    case 5: reg_pass<2, 1, INV, false, true>(x, 4, g, 0, 0, tw); break;
+    case 4: reg_pass<2, 0, INV, true, true>(x, 0, 0, 1, 0, tw); break;
+    default: reg_pass<2, 0, INV, true, false>(x, 0, 0, 5 - lg2, g >> lg2, tw); break;
   }
 }
 
@@ -844,8 +906,9 @@ QCE_DEV void fft256_pass1(double2 (&x)[16], int lg2, int g, const double2* tw) {
     default: reg_pass16<0, INV, true, false>(x, 0, 0, 7 - lg2, g >> lg2, tw); break;  // n1 bits 4-7, j = n1 bits < 4
   }
 }
+// pass 2 of every N >= 16 split: storage bits 3..0 of a lane's 16 points (bits >= 4 fixed)
 template <bool INV>
-QCE_DEV void fft256_pass2(double2 (&x)[16], int lg2, const double2* tw) {
+QCE_DEV void fft_pass_low4(double2 (&x)[16], int lg2, const double2* tw) {
   switch (lg2 >= 4 ? 4 : lg2) {  // segment A = n2 bits [0, min(lg2, 4)), B = n1 bits [lg2, 4)
     case 4: reg_pass16<4, INV, true, true>(x, 3, 0, 0, 0, tw); break;
     case 3: reg_pass16<3, INV, true, true>(x, 2, 0, 0, 0, tw); break;
@@ -859,6 +922,257 @@ QCE_DEV void fft256_pass2(double2 (&x)[16], int lg2, const double2* tw) {
 // t % 4 and accumulator register r (row hq + 4 r) give bits 0-3 = r + 4 (t % 4) -- exactly the 16 points a lane
 // holds after pass 2, so the spectra and Z never pass through LDS between the transforms and the filter.
 QCE_DEV int chunk256_bin(int t, int row) { return (((row & 3) + 4 * (t >> 2)) << 4) | ((row >> 2) + 4 * (t & 3)); }
+
+// Zero-mean models, N = 64 (cfg3): k_fft_wave's persistent one-wave-per-tile schedule with the transform in registers.
+// Pass 1 (storage bits 5, 4) runs on the prefetched y (lane: observations s0 + 4 q, positions g + 16 j), one
+// wave-local LDS exchange, pass 2 (bits 3..0) leaves lane (hq, col) holding positions 16 hq + i of observation col.
+// The tables are ordered so those 16 points are the lane's own operands: lp k-step u, k-index hq = position
+// 16 hq + u (the B operand |Y|^2 comes from registers, computed once per tile), filter tile t, row hq + 4 r =
+// position 16 hq + r + 4 t (chunk256_bin).  The spectra wait in the lane's own slots of the wave tile during the
+// component loop; Z, inverse pass 2, the exchange and inverse pass 1 run the same way back, stores from registers.
+template <int OUT>
+__global__ __launch_bounds__(256, 2) void k_fft_wreg(long long B, long long ntiles, int lg2, int Kp,
+                                                     const double2* __restrict__ y, const double* __restrict__ pr,
+                                                     const double* __restrict__ pc, const double* __restrict__ pw,
+                                                     double2* __restrict__ h, double* __restrict__ om,
+                                                     double* __restrict__ os, float* __restrict__ oa) {
+  constexpr int N = 64, NT = 4, NL = 8, NW = 8, RS = N + 1;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double2* tw = reinterpret_cast<double2*>(smem);
+  const int tid = threadIdx.x;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  double* etab = reinterpret_cast<double*>(tw + 128);  // 2^(j/32), j < 32
+  double2* T = tw + 128 + 16 + wid * (16 * RS);
+  for (int t = tid; t < 128; t += 256) {
+    double sn, cs;
+    sincospi(-(double)t / 128.0, &sn, &cs);
+    tw[t] = make_double2(cs, sn);
+  }
+  exp2_tab_init(etab, tid);
+  __syncthreads();
+  const int col = lane & 15, hq = lane >> 4;
+  const int g1 = lane & 15, s0 = lane >> 4;  // pass-1 lane: observations s0 + 4 q, positions g1 + 16 j
+  double2* Town = T + col * RS + 16 * hq;    // the lane's pass-2 points
+  const int ncb = Kp >> 4;
+  // tables, y and h through buffer descriptors (scalar registers); per-lane 32-bit offsets
+  const __amdgpu_buffer_rsrc_t rpr = buf_rsrc(pr, (unsigned)(Kp * N * 8)), rpw = buf_rsrc(pw, (unsigned)(Kp * N * 8));
+  const __amdgpu_buffer_rsrc_t rpc = buf_rsrc(pc, (unsigned)(Kp * 8));
+  const unsigned ul16 = (unsigned)lane * 16;
+  const unsigned yo = (unsigned)(s0 * N + g1) * 16;  // pass-1 lane: byte offset of (s0, g1) in a tile
+  FW_STAMP_DECL
+  const long long W = (long long)gridDim.x * 4;
+  const long long nmain = (ntiles / W) * W;
+  double2 v[16];  // y of a tile in the pass-1 layout: v[4 q + j] = y[s0 + 4 q][g1 + 16 j]
+  auto load_y = [&](long long t) __attribute__((always_inline)) {
+    const long long bb = t * 16;
+    const int rr = (int)((B - bb) < 16 ? (B - bb) : 16);
+    const __amdgpu_buffer_rsrc_t ry = buf_rsrc(y + bb * N, (unsigned)(rr * N * 16));  // rows past B read 0
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[4 * q + j] = buf_ld2(ry, yo + 256 * j, 4096 * q);
+  };
+  auto run_tile = [&](long long tile, int s0b, int bs, long long next, bool coop) __attribute__((always_inline)) {
+    const long long b0 = tile * 16;
+    const int rows = (int)((B - b0) < 16 ? (B - b0) : 16);
+    if (coop) load_y(tile);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      fft64_pass1<false>(v + 4 * q, lg2, g1, tw);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) T[(s0 + 4 * q) * RS + g1 + 16 * j] = v[4 * q + j];
+    }
+    wave_lds_sync();
+    FW_STAMP(0);
+    {
+      double2 yv[16];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) yv[i] = Town[i];
+      fft_pass_low4<false>(yv, lg2, tw);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) Town[i] = yv[i];  // the lane's own slots: no other lane reads them
+    }
+    // |Y|^2 of lp k-step u is the lane's own point u, re-derived from the spectra per use (two VALU per k-step keep
+    // 32 registers free for the next tile's y)
+    auto y2 = [&](int u, unsigned o) {
+      const double2 q = Town[u + o];
+      return q.x * q.x + q.y * q.y;
+    };
+    FW_STAMP(1);
+    f64x4 F[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+      for (int r = 0; r < 4; ++r) F[t][r] = 0.0;
+    double m = -__builtin_inf(), ssum = 0.0;
+    // c'_comp is added after the MFMAs, so its loads have the whole product to land
+    auto lp_block = [&](int cb, const double2* ta) {
+      double pcv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) pcv[r] = buf_ld1(rpc, (unsigned)(hq + 4 * r) * 8, (unsigned)cb * 128);
+      f64x4 C;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) C[r] = 0.0;
+      unsigned o = 0;  // opaque zero: the spectra reads stay in the loop instead of being hoisted into registers
+      asm volatile("" : "+v"(o));
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        C = mfma16x16x4d(ta[i].x, y2(2 * i, o), C);
+        C = mfma16x16x4d(ta[i].y, y2(2 * i + 1, o), C);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) C[r] += pcv[r];
+      return C;
+    };
+    // Softmax with a lagging shift m: the weights are e^(lp - m) with m moved (and F, s rescaled) only when a lane's
+    // block maximum exceeds it by more than 32 nats -- weights stay below e^32, and after the first blocks the
+    // rescale (one exp and 16 multiplies per block) is skipped by the whole wave
+    auto softmax = [&](const f64x4& C, double* e) {
+      const double bm = col_max4(fmax(fmax(C[0], C[1]), fmax(C[2], C[3])));
+      const bool up = bm > m + 32.0;
+      if (__builtin_amdgcn_ballot_w64(up)) {
+        const double mn = up ? bm : m;
+        const double alpha = exp_nonpos(m - mn, etab);  // 1 where the shift stays, 0 from -inf
+        ssum *= alpha;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) F[t] *= alpha;
+        m = mn;
+      }
+      const double sh = (m == -__builtin_inf()) ? 0.0 : m;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) e[r] = exp_nonpos(C[r] - sh, etab);
+      ssum += col_sum4((e[0] + e[1]) + (e[2] + e[3]));
+    };
+    auto filter_block = [&](const double2* tb, const double* e) {
+#pragma unroll
+      for (int j = 0; j < 4 * NT; ++j) {
+        const int r = j / NT, t = j % NT;
+        const double wv = (j & 1) ? tb[j >> 1].y : tb[j >> 1].x;
+        F[t] = mfma16x16x4d(wv, e[r], F[t]);
+      }
+    };
+    const int nb = (ncb - s0b + bs - 1) / bs;  // this wave's component blocks s0b + j bs, j < nb
+    auto blk = [&](int j) { return s0b + j * bs; };
+    if (nb > 0) {
+      const int last = nb - 1;
+      double2 ta[NL], tb[NW];
+#pragma unroll
+      for (int i = 0; i < NL; ++i) ta[i] = buf_ld2(rpr, ul16, (unsigned)blk(0) * NL * 1024 + 1024 * i);
+      f64x4 C = lp_block(blk(0), ta);
+      {
+        const int b1 = blk(last > 0 ? 1 : 0);
+#pragma unroll
+        for (int i = 0; i < NL; ++i) ta[i] = buf_ld2(rpr, ul16, (unsigned)b1 * NL * 1024 + 1024 * i);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) tb[i] = buf_ld2(rpw, ul16, (unsigned)blk(0) * NW * 1024 + 1024 * i);
+      }
+      FW_STAMP(2);
+      for (int j = 0; j < last; ++j) {
+        const int b1 = blk(j + 1), b2 = blk(j + 2 < last ? j + 2 : last);
+        const f64x4 Cn = lp_block(b1, ta);
+#pragma unroll
+        for (int i = 0; i < NL; ++i) ta[i] = buf_ld2(rpr, ul16, (unsigned)b2 * NL * 1024 + 1024 * i);
+        double e[4];
+        softmax(C, e);
+        filter_block(tb, e);
+#pragma unroll
+        for (int i = 0; i < NW; ++i) tb[i] = buf_ld2(rpw, ul16, (unsigned)b1 * NW * 1024 + 1024 * i);
+        C = Cn;
+      }
+      FW_STAMP(3);
+      if (next >= 0) load_y(next);  // behind the last block, the merge, the inverse transform and the store
+      {
+        double e[4];
+        softmax(C, e);
+        filter_block(tb, e);
+      }
+    }
+    if (coop) {  // waves 1-3 hand (F, m, s) to wave 0 through their own tiles (wave 0's holds its spectra)
+      double* Td = reinterpret_cast<double*>(T);
+      if (wid != 0) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) Td[(t * 4 + r) * 64 + lane] = F[t][r];
+        Td[4 * NT * 64 + lane] = m;
+        Td[(4 * NT + 1) * 64 + lane] = ssum;
+      }
+      __syncthreads();
+      if (wid == 0) {  // fixed order: wave 0's own partial, then waves 1, 2, 3
+        double mm = m;
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+          const double* Tw = reinterpret_cast<const double*>(tw + 128 + 16 + w * (16 * RS));
+          mm = fmax(mm, Tw[4 * NT * 64 + lane]);
+        }
+        const double f0 = exp_nonpos(m - mm, etab);
+        ssum *= f0;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) F[t] *= f0;
+#pragma unroll
+        for (int w = 1; w < 4; ++w) {
+          const double* Tw = reinterpret_cast<const double*>(tw + 128 + 16 + w * (16 * RS));
+          const double mw = Tw[4 * NT * 64 + lane];
+          const double fw = exp_nonpos(mw - mm, etab);
+          ssum = fma(Tw[(4 * NT + 1) * 64 + lane], fw, ssum);
+#pragma unroll
+          for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) F[t][r] = fma(Tw[(t * 4 + r) * 64 + lane], fw, F[t][r]);
+        }
+        m = mm;
+      }
+    }
+    if (!coop || wid == 0) {
+      const double sc = (OUT == 0) ? 1.0 / ssum : 1.0;
+      if ((OUT == 3 || OUT == 4) && hq == 0 && col < rows) {
+        om[b0 + col] = m;
+        os[b0 + col] = ssum;
+      }
+      double2 z[16];
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const double2 q = Town[r + 4 * t];
+          const double f = F[t][r] * sc;
+          z[r + 4 * t] = make_double2(q.x * f, q.y * f);
+        }
+      FW_STAMP(4);
+      fft_pass_low4<true>(z, lg2, tw);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) Town[i] = z[i];
+      wave_lds_sync();
+      const unsigned ob = (unsigned)rows * N * 16;  // rows past B: stores dropped by the descriptor extent
+      const __amdgpu_buffer_rsrc_t ro = (OUT == 0) ? buf_rsrc(h + b0 * N, ob)
+                                      : (OUT == 3) ? buf_rsrc(reinterpret_cast<float2*>(oa) + b0 * N, ob / 2)
+                                                   : buf_rsrc(reinterpret_cast<double2*>(oa) + b0 * N, ob);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double2 x[4];
+        const int sr = s0 + 4 * q;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) x[j] = T[sr * RS + g1 + 16 * j];
+        fft64_pass1<true>(x, lg2, g1, tw);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (OUT == 3)
+            buf_st1f2(make_float2((float)x[j].x, (float)x[j].y), ro, yo / 2 + 128 * j, 2048 * q);
+          else
+            buf_st2(x[j], ro, yo + 256 * j, 4096 * q);
+        }
+      }
+      FW_STAMP(5);
+    }
+    if (coop) __syncthreads();  // wave 0 has read the partials before the next tile overwrites them
+    wave_lds_sync();
+    FW_STAMP(6);
+  };
+  long long tile = (long long)blockIdx.x * 4 + wid;
+  if (tile < nmain) load_y(tile);
+  for (; tile < nmain; tile += W) run_tile(tile, 0, 1, tile + W < nmain ? tile + W : -1, false);
+  for (long long tt = nmain + blockIdx.x; tt < ntiles; tt += gridDim.x) run_tile(tt, wid, 4, -1, true);
+  FW_STAMP_FLUSH
+}
 
 // Zero-mean models, N = 128, 256: one workgroup (4 waves) per 16 observations, the components split over the waves
 // for the log-probabilities and the bins split over the waves for the filter, so the softmax of every (component,
@@ -938,7 +1252,7 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < 16; ++i) yv[i] = T[col * RS + 16 * (hq + 4 * wid) + i];
-    fft256_pass2<false>(yv, lg2, tw);
+    fft_pass_low4<false>(yv, lg2, tw);
     FW_STAMP(1);
     __syncthreads();  // every spectrum value is in registers: the tile takes |Y|^2, e and the column statistics
     // |Y|^2 in the lp B layout (k-step u = p / 4 covers p = 4 u + hq'): position 16 (hq + 4 w) + r + 4 t is k-step
@@ -1123,7 +1437,7 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
         const double f = F[t][r] * sc;
         yv[4 * t + r] = make_double2(yv[4 * t + r].x * f, yv[4 * t + r].y * f);
       }
-    fft256_pass2<true>(yv, lg2, tw);
+    fft_pass_low4<true>(yv, lg2, tw);
 #pragma unroll
     for (int i = 0; i < 16; ++i) T[col * RS + 16 * (hq + 4 * wid) + i] = yv[i];
     __syncthreads();
@@ -1206,6 +1520,9 @@ __global__ __launch_bounds__(256) void k_fft_pack(int N, int lg1, int lg2, int K
   const int n2m = (1 << lg2) - 1;
   auto bin_of = [&](int p) { return (brev(p >> lg2, lg1) << lg2) | brev(p & n2m, lg2); };
   const long long total = (long long)N * Kp;
+  // fragment order, table layouts: 0 k_fft_wave (lp bins 4 t + k, filter bins 16 t + row), 1 k_fft_chunk<256> (filter
+  // bins chunk256_bin), 2 k_fft_wreg (lp bins 16 k + t, filter bins chunk256_bin)
+  const int layout = (N == 256) ? 1 : (N == 64 && !has_mean && frag) ? 2 : 0;
   if (N <= 64 || (!has_mean && frag)) {  // fragment order: e = ((cb Q + i) 64 + lane) 2 + s, Q = N / 8 16-byte loads per block and table
     const int Q = N / 8, NT = N / 16;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
@@ -1215,7 +1532,7 @@ __global__ __launch_bounds__(256) void k_fft_pack(int N, int lg1, int lg2, int K
       const int i = (int)(g % Q), cb = (int)(g / Q);
       const int j = 2 * i + s;
       {  // lp: t = j, bin 4t + lane/16, comp 16cb + lane%16
-        const int p = 4 * j + (lane >> 4), k = 16 * cb + (lane & 15);
+        const int p = (layout == 2) ? 16 * (lane >> 4) + j : 4 * j + (lane >> 4), k = 16 * cb + (lane & 15);
         const bool ok = k < K;
         const long long src = (long long)bin_of(p) * K + k;
         pr[e] = ok ? -rinvT[src] : 0.0;
@@ -1227,7 +1544,7 @@ __global__ __launch_bounds__(256) void k_fft_pack(int N, int lg1, int lg2, int K
       {  // filter: r = j / NT, t = j % NT; comp 16cb + lane/16 + 4r, bin 16t + lane%16
         const int r = j / NT, t = j % NT;
         const int k = 16 * cb + (lane >> 4) + 4 * r;
-        const int p = (N == 256) ? chunk256_bin(t, lane & 15) : 16 * t + (lane & 15);
+        const int p = (layout != 0) ? chunk256_bin(t, lane & 15) : 16 * t + (lane & 15);
         const bool ok = k < K;
         const long long src = (long long)k * N + bin_of(p);
         pw[e] = ok ? wT[src] : 0.0;
@@ -1310,8 +1627,29 @@ hipError_t launch_wave_c(const QceFftEstArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int OUT>
+hipError_t launch_wreg(const QceFftEstArgs& a, hipStream_t st) {
+  const size_t lds = 128 * 16 + 32 * 8 + (size_t)4 * 16 * 65 * 16;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_fft_wreg<OUT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const long long ntiles = (a.B + 15) / 16;
+  const long long slots = 2LL * (a.cu > 0 ? a.cu : 256);  // persistent: two workgroups (8 waves) per CU
+  const long long wgs = ntiles < slots ? ntiles : slots;
+  hipLaunchKernelGGL((k_fft_wreg<OUT>), dim3((unsigned)wgs), dim3(256), lds, st, a.B, ntiles, __builtin_ctz(a.n2), a.Kp,
+                     a.y, a.pr, a.pc, a.pw, a.h, a.om, a.os, a.oa);
+  return hipGetLastError();
+}
+
 template <int N, int OUT, bool HM>
 hipError_t launch_wave_t(const QceFftEstArgs& a, hipStream_t st) {
+  if constexpr (N == 64 && !HM) {
+    if (a.chunk) return launch_wreg<OUT>(a, st);
+  }
   return a.n1 == 1 ? launch_wave_c<N, OUT, HM, true>(a, st) : launch_wave_c<N, OUT, HM, false>(a, st);
 }
 

@@ -453,11 +453,17 @@ def test_fourier_mfma_kernel_vs_lds_kernel(K, N, blocks, B, n_bits, mean, monkey
     (64, 256, None, 100, 2),        # circulant 256: both register passes on one axis
     (40, 256, (2, 128), 90, 3),     # pass 1 = 3 bits of n2 + the n1 bit
     (48, 256, (64, 4), 77, 2),      # n2 = 4: pass 2 = both n2 bits + 2 low n1 bits, pass 1 n1 only (j != 0)
+    # N = 64: k_fft_wreg (register transform, persistent one-wave tiles + cooperative tail)
+    (128, 64, None, 3001, 3),       # cfg3 geometry, circulant: pass 1 = n2 bits 5, 4
+    (64, 64, (2, 32), 500, 2),      # pass 1 = n2 bit 4 + the n1 bit
+    (48, 64, (4, 16), 400, 2),      # pass 1 = both n1 bits, j = 0
+    (40, 64, (16, 4), 300, 1),      # n2 = 4: pass 1 on n1 with j != 0, pass 2 mixes both axes
 ])
 def test_fourier_chunk_kernel(K, N, blocks, B, n_bits, monkeypatch):
     """k_fft_chunk (zero-mean N = 128, 256: components split over the waves for lp / softmax, bins for the
-    filter, two barriers per 128-component chunk) against the FP64 oracle and the bin-split k_fft_mfma
-    (QCE_FFT_CHUNK=0), 'all' mode and both K-shard partial accumulators."""
+    filter, two barriers per 128-component chunk) and k_fft_wreg (zero-mean N = 64) against the FP64 oracle and
+    the kernels they replace (QCE_FFT_CHUNK=0: bin-split k_fft_mfma, LDS-transform k_fft_wave), 'all' mode and
+    both K-shard partial accumulators."""
     _gpu_or_skip()
     from oracle import qce_oracle as O
     from quantized_channel_estimation_amd import _lib, inputs

@@ -41,8 +41,11 @@ def main():
     st = buf[:n].reshape(-1, 8).astype(np.float64)
     st = st[st.sum(1) > 0]
     tot = st.sum(1)
-    if cfg["N"] >= 128 and os.environ.get("QCE_FFT_CHUNK", "1") != "0":  # k_fft_chunk (zero-mean N = 128, 256)
+    new = os.environ.get("QCE_FFT_CHUNK", "1") != "0"
+    if cfg["N"] >= 128 and new:  # k_fft_chunk (zero-mean N = 128, 256)
         names = ["y load", "FFT fwd", "Y regs+|Y|^2", "lp MFMA", "max/e/sums", "filter", "Z+IFFT", "store"]
+    elif cfg["N"] == 64 and new:  # k_fft_wreg
+        names = ["pass1+xchg", "pass2+stash", "lp0", "loop", "last+Z", "IFFT+store", "sync", "-"]
     else:  # k_fft_wave; k_fft_mfma: 2 = Y regs + lp0, 3 = loop, 4 = Z
         names = ["y load", "FFT fwd", "y2+lp0", "loop", "last+Z", "FFT inv", "store", "-"]
     print(f"waves {st.shape[0]}, mean cycles/wave {tot.mean():.4g} (min {tot.min():.4g}, max {tot.max():.4g})")

@@ -19,6 +19,6 @@ run lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_LDS || 
 run tcc TCC_HIT_sum TCC_MISS_sum || exit $?
 run inst SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_MFMA SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM GRBM_GUI_ACTIVE || exit $?
 cd $R
-python3 tools/pmc_summary_fft.py $OUT > $OUT/summary.txt 2>&1
+python3 tools/pmc_summary_fft.py $OUT ${KPAT:-k_fft_chunk} > $OUT/summary.txt 2>&1
 cat $OUT/summary.txt
 find $OUT/stats -name '*kernel_stats.csv' -exec head -6 {} \; | cut -c1-200
