@@ -269,7 +269,7 @@ def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
         fft_flops = (4.0 * k_local * N + 10.0 * N * math.log2(N)) * B  # D3: zero-mean FFT-path flops
         return dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
-                    kernel="k_fft_wave" if N <= 64 else "k_fft_mfma",
+                    kernel=fourier_kernel(N, dm_has_mean(dm)),
                     structure=f"block-circulant ({n1},{n2})" if n1 > 1 else "circulant",
                     kernel_ms=round(kern_ms, 4), bytes_per_launch=bytes_per_launch,
                     fp64_flops_per_launch=fft_flops, fp64_tflops=round(fft_flops / (kern_ms * 1e-3) / 1e12, 3),
@@ -311,10 +311,20 @@ def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
                 mfma_issue_frac=round(ex / (kern_ms * 1e-3) / 1e12 / FP16_MFMA_PEAK_TFLOPS, 4))
 
 
+def fourier_kernel(N, has_mean):
+    """The Fourier-path kernel qce_fft_mfma.hip runs for this shape (QCE_FFT_CHUNK=0 selects the round-2 kernels)."""
+    new = os.environ.get("QCE_FFT_CHUNK", "1") != "0" and not has_mean
+    if N == 64 and new:
+        return "k_fft_wreg"
+    if N <= 64:
+        return "k_fft_wave"
+    return "k_fft_chunk" if new else "k_fft_mfma"
+
+
 def dtype_of(dm):
     if dm.structure()[2]:
         return "f64"
-    if dm.precision == "f64" and dm.N <= 128:
+    if dm.precision == "f64":  # k_est_all_f64 up to padded 128, k_lp_f64 + k_wsum_f64 beyond
         return "f64"
     return "f16x2 (fp16 hi+lo split, fp32 accumulate, fp64 softmax)"
 
