@@ -91,10 +91,96 @@ __global__ __launch_bounds__(256) void k_zgemm(int m, int n, int k, double2 alph
     }
 }
 
+// The same batched complex GEMM on FP64 MFMA: the 32x32 output tile of a workgroup is four 16x16 wave tiles; per
+// k-step of 4 a wave issues the four real products of the complex one, Re += Ar Br - Ai Bi, Im += Ar Bi + Ai Br
+// (v_mfma_f64_16x16x4_f64, FP64 accumulation), its operands read from the same LDS staging as k_zgemm.
+template <int OPA, int OPB>
+__global__ __launch_bounds__(256) void k_zgemm_mfma(int m, int n, int k, double2 alpha, const double2* __restrict__ A,
+                                                    int lda, long long sA, const double2* __restrict__ B, int ldb,
+                                                    long long sB, double2 beta, double2* __restrict__ C, int ldc,
+                                                    long long sC) {
+  __shared__ double2 As[16][33];
+  __shared__ double2 Bs[16][33];
+  const int z = blockIdx.z;
+  A += z * sA;
+  B += z * sB;
+  C += z * sC;
+  const int row0 = blockIdx.y * 32, col0 = blockIdx.x * 32;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wy = wv >> 1, wx = wv & 1, q = lane >> 4, c16 = lane & 15;
+  f64x4 accr = {0.0, 0.0, 0.0, 0.0}, acci = {0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < k; k0 += 16) {
+    for (int e = tid; e < 512; e += 256) {
+      int i, l;
+      double2 v = make_double2(0.0, 0.0);
+      if (OPA == 0) {
+        l = e & 15;
+        i = e >> 4;
+        if (row0 + i < m && k0 + l < k) v = A[(long long)(row0 + i) * lda + k0 + l];
+      } else {
+        i = e & 31;
+        l = e >> 5;
+        if (row0 + i < m && k0 + l < k) v = A[(long long)(k0 + l) * lda + row0 + i];
+        if (OPA == 2) v.y = -v.y;
+      }
+      As[l][i] = v;
+      int j;
+      v = make_double2(0.0, 0.0);
+      if (OPB == 0) {
+        j = e & 31;
+        l = e >> 5;
+        if (k0 + l < k && col0 + j < n) v = B[(long long)(k0 + l) * ldb + col0 + j];
+      } else {
+        l = e & 15;
+        j = e >> 4;
+        if (k0 + l < k && col0 + j < n) v = B[(long long)(col0 + j) * ldb + k0 + l];
+        if (OPB == 2) v.y = -v.y;
+      }
+      Bs[l][j] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const double2 a = As[4 * kk + q][16 * wy + c16];  // A operand: row = lane % 16, k = lane / 16
+      const double2 b = Bs[4 * kk + q][16 * wx + c16];  // B operand: k = lane / 16, col = lane % 16
+      accr = mfma16x16x4d(a.x, b.x, accr);
+      accr = mfma16x16x4d(-a.y, b.y, accr);
+      acci = mfma16x16x4d(a.x, b.y, acci);
+      acci = mfma16x16x4d(a.y, b.x, acci);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {  // D layout: row = lane / 16 + 4 r, col = lane % 16
+    const int rr = row0 + 16 * wy + q + 4 * r, cc = col0 + 16 * wx + c16;
+    if (rr < m && cc < n) {
+      double2* p = C + (long long)rr * ldc + cc;
+      double2 v = cmul(alpha, make_double2(accr[r], acci[r]));
+      if (beta.x != 0.0 || beta.y != 0.0) v = cadd(v, cmul(beta, *p));
+      *p = v;
+    }
+  }
+}
+
 static hipError_t zgemm(int opa, int opb, int m, int n, int k, double2 alpha, const double2* A, int lda, long long sA,
                         const double2* B, int ldb, long long sB, double2 beta, double2* C, int ldc, long long sC,
                         int batch, hipStream_t st) {
   dim3 grid((n + 31) / 32, (m + 31) / 32, batch);
+  static const bool valu = [] {  // QCE_ZGEMM=valu: the VALU kernel (A/B runs)
+    const char* e = getenv("QCE_ZGEMM");
+    return e && strcmp(e, "valu") == 0;
+  }();
+  if (!valu) {
+#define ZM(OA, OB)                                                                                                 \
+  if (opa == OA && opb == OB) {                                                                                    \
+    hipLaunchKernelGGL((k_zgemm_mfma<OA, OB>), grid, dim3(256), 0, st, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, \
+                       C, ldc, sC);                                                                                \
+    return hipGetLastError();                                                                                      \
+  }
+    ZM(0, 0) ZM(0, 2) ZM(2, 0) ZM(0, 1)
+#undef ZM
+    return hipErrorInvalidValue;
+  }
 #define ZG(OA, OB)                                                                                              \
   if (opa == OA && opb == OB) {                                                                                 \
     hipLaunchKernelGGL((k_zgemm<OA, OB>), grid, dim3(256), 0, st, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, \
