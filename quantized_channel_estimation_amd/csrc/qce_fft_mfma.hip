@@ -1192,7 +1192,7 @@ struct FftChunkLds {
   static constexpr size_t tile = (size_t)TS * RS * 16;
   static constexpr size_t y2 = (size_t)N * TS * 8, e = (size_t)128 * TS * 8, sm = (size_t)2 * 4 * TS * 8;
   static constexpr size_t body = tile > y2 + e + sm ? tile : y2 + e + sm;
-  static constexpr size_t bytes = 128 * 16 + body;
+  static constexpr size_t bytes = 128 * 16 + body + 32 * 8;  // + the exp table
 };
 
 template <int N, int OUT>
@@ -1215,6 +1215,7 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
   double2* Y2 = T;                                                 // [N/8][4][16] (k-steps 2i, 2i+1 of the lp B)
   double2* E = reinterpret_cast<double2*>(reinterpret_cast<double*>(T) + N * TS);  // [CB * 2][4][16]
   double* SM = reinterpret_cast<double*>(E + CB * 2 * 64);         // [2][4][16] column maxima, column sums
+  double* etab = reinterpret_cast<double*>(smem) + 2 * 128 + FftChunkLds<N>::body / 8;  // 2^(j/32), after the body
   const int tid = threadIdx.x;
   const long long b0 = (long long)blockIdx.x * TS;
   const int rows = (int)((B - b0) < TS ? (B - b0) : TS);
@@ -1239,6 +1240,7 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
         sincospi(-(double)t / 128.0, &sn, &cs);
         tw[t] = make_double2(cs, sn);
       }
+      exp2_tab_init(etab, tid);
       __syncthreads();
       FW_STAMP(0);
       if (s1 >= rows) {
@@ -1272,6 +1274,7 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
       sincospi(-(double)t / 128.0, &sn, &cs);
       tw[t] = make_double2(cs, sn);
     }
+    exp2_tab_init(etab, tid);
     {  // all loads in flight at once; rows past the batch end read a clamped (valid) row and are stored as 0
       constexpr int NLY = TS * N / 256;
       const double2* yt = y + b0 * N;
@@ -1321,8 +1324,9 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
     for (int r = 0; r < 4; ++r) F[t][r] = 0.0;
   double m = -__builtin_inf(), ssum = 0.0;
   const int ncb = Kp >> 4;
-  const double2* PR = reinterpret_cast<const double2*>(pr) + lane;
-  const double2* PW = reinterpret_cast<const double2*>(pw) + lane;
+  // tables through buffer descriptors: scalar block offsets, one 32-bit lane offset (no 64-bit address math)
+  const __amdgpu_buffer_rsrc_t rpr = buf_rsrc(pr, (unsigned)(Kp * N * 8)), rpw = buf_rsrc(pw, (unsigned)(Kp * N * 8));
+  const unsigned ul16 = (unsigned)lane * 16;
   const double2* Y2l = Y2 + hq * 16 + col;
   for (int c0 = 0; c0 < ncb; c0 += CB) {
     const int cb0 = c0 + wid, cb1 = cb0 + 4;
@@ -1334,21 +1338,20 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
       C1[r] = v1 ? pc[16 * cb1 + hq + 4 * r] : -__builtin_inf();
     }
     if (v1) {
-      const double2* A0 = PR + (long long)cb0 * NL * 64;
-      const double2* A1 = PR + (long long)cb1 * NL * 64;
+      const unsigned o0 = (unsigned)cb0 * NL * 1024, o1 = (unsigned)cb1 * NL * 1024;
 #pragma unroll
       for (int i = 0; i < NL; ++i) {
-        const double2 a0 = A0[i * 64], a1 = A1[i * 64], b = Y2l[i * 64];
+        const double2 a0 = buf_ld2(rpr, ul16, o0 + 1024 * i), a1 = buf_ld2(rpr, ul16, o1 + 1024 * i), b = Y2l[i * 64];
         C0 = mfma16x16x4d(a0.x, b.x, C0);
         C1 = mfma16x16x4d(a1.x, b.x, C1);
         C0 = mfma16x16x4d(a0.y, b.y, C0);
         C1 = mfma16x16x4d(a1.y, b.y, C1);
       }
     } else if (v0) {
-      const double2* A0 = PR + (long long)cb0 * NL * 64;
+      const unsigned o0 = (unsigned)cb0 * NL * 1024;
 #pragma unroll
       for (int i = 0; i < NL; ++i) {
-        const double2 a0 = A0[i * 64], b = Y2l[i * 64];
+        const double2 a0 = buf_ld2(rpr, ul16, o0 + 1024 * i), b = Y2l[i * 64];
         C0 = mfma16x16x4d(a0.x, b.x, C0);
         C0 = mfma16x16x4d(a0.y, b.y, C0);
       }
@@ -1361,19 +1364,19 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
     __syncthreads();
     const double mn = fmax(fmax(m, fmax(SM[col], SM[16 + col])), fmax(SM[32 + col], SM[48 + col]));
     const double sh = (mn == -__builtin_inf()) ? 0.0 : mn;
-    const double alpha = exp(m - sh);
+    const double alpha = exp_nonpos(m - sh, etab);
     // e of the wave's own components, in the filter's B layout: k-step ks = 4 (local block) + r covers the
     // components 4 ks + hq; pair (ks even, ks + 1) per 16-byte slot
     double ls = 0.0;
     {
       double e[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) e[r] = v0 ? exp(C0[r] - sh) : 0.0;
+      for (int r = 0; r < 4; ++r) e[r] = v0 ? exp_nonpos(C0[r] - sh, etab) : 0.0;
       ls += (e[0] + e[1]) + (e[2] + e[3]);
       E[((2 * wid) * 4 + hq) * 16 + col] = make_double2(e[0], e[1]);
       E[((2 * wid + 1) * 4 + hq) * 16 + col] = make_double2(e[2], e[3]);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) e[r] = v1 ? exp(C1[r] - sh) : 0.0;
+      for (int r = 0; r < 4; ++r) e[r] = v1 ? exp_nonpos(C1[r] - sh, etab) : 0.0;
       ls += (e[0] + e[1]) + (e[2] + e[3]);
       E[((2 * (wid + 4)) * 4 + hq) * 16 + col] = make_double2(e[0], e[1]);
       E[((2 * (wid + 4) + 1) * 4 + hq) * 16 + col] = make_double2(e[2], e[3]);
@@ -1387,24 +1390,20 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
 #pragma unroll
     for (int t = 0; t < NTW; ++t) F[t] *= alpha;
     // filter over the chunk's blocks (padding blocks beyond ncb carry e = 0 and are skipped)
-    // the operands of block bl + 1 are fetched while block bl computes
+    // the operands of block bl + 1 are fetched while block bl computes; the CB blocks are unrolled (guards are
+    // wave-uniform), so the two operand buffers alternate without register copies
     const int nbl = (ncb - c0) < CB ? (ncb - c0) : CB;
     constexpr int NWL = 2 * NTW;  // 16-byte filter operand loads per block and wave: (r, tile pair tp)
-    const double2* Wb = PW + (long long)c0 * NWF * 64 + ((wid * NTW) >> 1) * 64;
+    const unsigned wbase = (unsigned)c0 * NWF * 1024 + (unsigned)((wid * NTW) >> 1) * 1024;
     auto load_w = [&](int bl, double2 (&wv)[NWL]) {
-      const double2* W = Wb + (long long)bl * NWF * 64;
+      const unsigned ob = wbase + (unsigned)bl * NWF * 1024;
 #pragma unroll
       for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int tp = 0; tp < NTW / 2; ++tp) wv[r * (NTW / 2) + tp] = W[((r * NTF) >> 1) * 64 + tp * 64];
+        for (int tp = 0; tp < NTW / 2; ++tp)
+          wv[r * (NTW / 2) + tp] = buf_ld2(rpw, ul16, ob + ((r * NTF) >> 1) * 1024 + tp * 1024);
     };
-    double2 wn[NWL];
-    load_w(0, wn);
-    for (int bl = 0; bl < nbl; ++bl) {
-      double2 wc[NWL];
-#pragma unroll
-      for (int i = 0; i < NWL; ++i) wc[i] = wn[i];
-      if (bl + 1 < nbl) load_w(bl + 1, wn);
+    auto filter_blk = [&](int bl, const double2 (&wc)[NWL]) {
 #pragma unroll
       for (int rp = 0; rp < 2; ++rp) {
         const double2 ev = E[((2 * bl + rp) * 4 + hq) * 16 + col];
@@ -1419,6 +1418,19 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
             F[2 * tp + 1] = mfma16x16x4d(wv.y, eb, F[2 * tp + 1]);
           }
         }
+      }
+    };
+    double2 wa[NWL], wb[NWL];
+    load_w(0, wa);
+#pragma unroll
+    for (int bl = 0; bl < CB; bl += 2) {
+      if (bl < nbl) {
+        if (bl + 1 < nbl) load_w(bl + 1, wb);
+        filter_blk(bl, wa);
+      }
+      if (bl + 1 < nbl) {
+        if (bl + 2 < nbl) load_w(bl + 2, wa);
+        filter_blk(bl + 1, wb);
       }
     }
     FW_STAMP(5);
