@@ -774,13 +774,15 @@ QCE_DEV void buf_st1f2(float2 v, __amdgpu_buffer_rsrc_t r, unsigned voff, unsign
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(qce_u32x2, v), r, voff, soff, 0);
 }
 
-// e^x for x <= 700 (x = -inf and x < -708 give 0, a weight below 1e-307 of the largest): 2^(k/32) from a 32-entry LDS
+// e^x for x <= 700 (x = -inf and x < -708 give e^-708 = 3e-308, negligible beside the largest weight 1, which every
+// use has): 2^(k/32) from a 32-entry LDS
 // table (exp2_tab, 2^(j/32)) times the degree-6 Taylor polynomial of e^r, |r| <= ln2/64 (truncation 4e-18), 2^(k>>5)
 // added to the exponent field: 18 VALU against ~32 for the libm exp, about 2 ulp.
 QCE_DEV double exp_nonpos(double x, const double* __restrict__ tab) {
   constexpr double L32 = 46.166241308446828384;      // 32 / ln 2
   constexpr double LH = 2.1660849390173098072e-02;   // ln 2 / 32, leading bits
   constexpr double LL = 2.3251928468788740148e-12;   // ln 2 / 32 - LH
+  x = fmax(x, -708.0);  // -inf and deep underflow -> e^-708 (3e-308, negligible beside the largest weight 1)
   const double kf = __builtin_rint(x * L32);
   double r = fma(kf, -LH, x);
   r = fma(kf, -LL, r);
@@ -792,8 +794,7 @@ QCE_DEV double exp_nonpos(double x, const double* __restrict__ tab) {
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);
   const double v = tab[k & 31] * p;
-  const double res = __hiloint2double(__double2hiint(v) + ((k >> 5) << 20), __double2loint(v));
-  return (x < -708.0) ? 0.0 : res;
+  return __hiloint2double(__double2hiint(v) + ((k >> 5) << 20), __double2loint(v));
 }
 QCE_DEV void exp2_tab_init(double* tab, int tid) {
   if (tid < 32) tab[tid] = exp2((double)tid / 32.0);
@@ -1025,13 +1026,14 @@ __global__ __launch_bounds__(256, 2) void k_fft_wreg(long long B, long long ntil
     };
     // Softmax with a lagging shift m: the weights are e^(lp - m) with m moved (and F, s rescaled) only when a lane's
     // block maximum exceeds it by more than 32 nats -- weights stay below e^32, and after the first blocks the
-    // rescale (one exp and 16 multiplies per block) is skipped by the whole wave
+    // whole wave skips the rescale (column maximum, one exp, 16 multiplies).  ssum is the lane's own partial sum
+    // (its 4 components of each block); the column sum is taken once per tile.
     auto softmax = [&](const f64x4& C, double* e) {
-      const double bm = col_max4(fmax(fmax(C[0], C[1]), fmax(C[2], C[3])));
-      const bool up = bm > m + 32.0;
-      if (__builtin_amdgcn_ballot_w64(up)) {
-        const double mn = up ? bm : m;
-        const double alpha = exp_nonpos(m - mn, etab);  // 1 where the shift stays, 0 from -inf
+      const double lm = fmax(fmax(C[0], C[1]), fmax(C[2], C[3]));
+      if (__builtin_amdgcn_ballot_w64(lm > m + 32.0)) {
+        const double bm = col_max4(lm);
+        const double mn = (bm > m + 32.0) ? bm : m;  // the column's four lanes agree (same bm, same m)
+        const double alpha = exp_nonpos(m - mn, etab);  // 1 where the shift stays, ~0 from -inf
         ssum *= alpha;
 #pragma unroll
         for (int t = 0; t < NT; ++t) F[t] *= alpha;
@@ -1040,7 +1042,7 @@ __global__ __launch_bounds__(256, 2) void k_fft_wreg(long long B, long long ntil
       const double sh = (m == -__builtin_inf()) ? 0.0 : m;
 #pragma unroll
       for (int r = 0; r < 4; ++r) e[r] = exp_nonpos(C[r] - sh, etab);
-      ssum += col_sum4((e[0] + e[1]) + (e[2] + e[3]));
+      ssum += (e[0] + e[1]) + (e[2] + e[3]);
     };
     auto filter_block = [&](const double2* tb, const double* e) {
 #pragma unroll
@@ -1086,6 +1088,7 @@ __global__ __launch_bounds__(256, 2) void k_fft_wreg(long long B, long long ntil
         filter_block(tb, e);
       }
     }
+    ssum = col_sum4(ssum);  // the lanes' partial sums -> the column's (bit-identical in its four lanes)
     if (coop) {  // waves 1-3 hand (F, m, s) to wave 0 through their own tiles (wave 0's holds its spectra)
       double* Td = reinterpret_cast<double*>(T);
       if (wid != 0) {
