@@ -236,10 +236,13 @@ __global__ __launch_bounds__(256) void k_gain_cr(int M, int N, const double2* __
                                                  double2* __restrict__ Aeff, int kind, int n_bits, int quant_kind,
                                                  double delta, const double* __restrict__ thr,
                                                  const double* __restrict__ lab, int beta_first) {
-  const int k = blockIdx.x, tid = threadIdx.x;
+  // grid (K, S): slice s of component k handles the rows i = s (mod S) of Cr, mu_y and Aeff; every slice derives
+  // all M gains itself (the beta-mix needs their mean), slice 0 stores them
+  const int k = blockIdx.x, tid = threadIdx.x, sl = blockIdx.y, S = gridDim.y;
   const double2* cy = Cy + (long long)k * M * M;
   double2* cr = Cr + (long long)k * M * M;
-  double* g = gain + (long long)k * M;
+  double* gout = gain + (long long)k * M;
+  __shared__ double g[256], pinv[256];
   __shared__ double s_beta;
   const double PI = 3.14159265358979323846;
   for (int i = tid; i < M; i += 256) {
@@ -269,6 +272,8 @@ __global__ __launch_bounds__(256) void k_gain_cr(int M, int N, const double2* __
       gi = 0.0;
     }
     g[i] = gi;
+    pinv[i] = 1.0 / sqrt(d);
+    if (sl == 0) gout[i] = gi;
   }
   __syncthreads();
   if (tid == 0) {
@@ -280,13 +285,13 @@ __global__ __launch_bounds__(256) void k_gain_cr(int M, int N, const double2* __
   __syncthreads();
   const double beta2 = s_beta * s_beta;
   const double two_over_pi = 2.0 / PI;
-  for (long long e = tid; e < (long long)M * M; e += 256) {
-    int i = (int)(e / M), j = (int)(e % M);
+  for (int i = sl + S * (tid >> 6); i < M; i += 4 * S)  // a wave per row, its lanes over the columns
+    for (int j = tid & 63; j < M; j += 64) {
+    const long long e = (long long)i * M + j;
     double2 v = cy[e];
     double2 o;
     if (kind == 0) {  // arcsine law (:292-301)
-      double pi_ = 1.0 / sqrt(cy[(long long)i * M + i].x);
-      double pj_ = 1.0 / sqrt(cy[(long long)j * M + j].x);
+      const double pi_ = pinv[i], pj_ = pinv[j];
       double re = (pi_ * v.x) * pj_, im = (pi_ * v.y) * pj_;
       re = re > 1.0 ? 1.0 : (re < -1.0 ? -1.0 : re);
       im = im > 1.0 ? 1.0 : (im < -1.0 ? -1.0 : im);
@@ -298,18 +303,16 @@ __global__ __launch_bounds__(256) void k_gain_cr(int M, int N, const double2* __
       if (i == j) o = make_double2(o.x + (1.0 - beta2) * v.x, o.y + (1.0 - beta2) * v.y);
     }
     cr[e] = o;
-  }
-  // mu_y = g * (A mu_k);  Aeff = diag(g) A
+    }
+  // mu_y = g * (A mu_k);  Aeff = diag(g) A  (the slice's rows)
   const double2* mu = means + (long long)k * N;
-  for (int i = tid; i < M; i += 256) {
+  for (int i = sl + S * tid; i < M; i += 256 * S) {
     double2 am = make_double2(0.0, 0.0);
     for (int n = 0; n < N; ++n) am = cfma(A[(long long)i * N + n], mu[n], am);
     means_y[(long long)k * M + i] = cscale(am, g[i]);
   }
-  for (long long e = tid; e < (long long)M * N; e += 256) {
-    int i = (int)(e / N);
-    Aeff[(long long)k * M * N + e] = cscale(A[e], g[i]);
-  }
+  for (int i = sl + S * (tid >> 6); i < M; i += 4 * S)
+    for (int n = tid & 63; n < N; n += 64) Aeff[(long long)k * M * N + (long long)i * N + n] = cscale(A[(long long)i * N + n], g[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -768,7 +771,9 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
     hipLaunchKernelGGL(k_diag_add, dim3((K * M + 255) / 256), dim3(256), 0, st, M, K, p.Cy, p.sigma2);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_gain_cr, dim3(K), dim3(256), 0, st, M, N, p.Cy, p.Cr, p.gain, p.A, p.means, p.means_y, p.Aeff,
+  // row slices per component: 4 where the gains are cheap to derive in every slice (1 bit, infinite resolution)
+  const unsigned gslices = (p.kind == 0 || p.kind == 2) ? 4u : 1u;
+  hipLaunchKernelGGL(k_gain_cr, dim3(K, gslices), dim3(256), 0, st, M, N, p.Cy, p.Cr, p.gain, p.A, p.means, p.means_y, p.Aeff,
                      p.kind, p.n_bits, p.quant_kind, p.delta, p.thr, p.lab, p.beta_first);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // M <= 64: QCE_CHOL = lds (default) | tri | wave picks the factorisation kernel (A/B runs; metric config,
