@@ -386,18 +386,21 @@ __global__ __launch_bounds__(256) void k_chol_inv(int M, double2* __restrict__ L
 }
 
 // Same factorisation with the matrix and its inverse resident in LDS (M <= 64: 2 x 64 KB), one
-// workgroup per component.  Scaling is deferred so every step is ONE barrier phase:
-//   factor  step j:  a_rc -= a_rj conj(a_cj) / a_jj   (r >= c > j; column j and a_jj are final)
-//           afterwards L_ij = a_ij / sqrt(a_jj)
-//   inverse step k:  X~_ic -= a_ik / a_kk * X~_kc      (i > k, c <= k; row k of X~ is final)
-//           afterwards Linv_ic = X~_ic / sqrt(a_ii)
-// (reads and writes of a step touch disjoint entries, so no second barrier is needed).
+// workgroup per component.  Scaling is deferred so every step j is ONE barrier phase that advances both:
+//   factor  :  a_rc -= a_rj conj(a_cj) / a_jj   (r >= c > j; column j and a_jj are final)
+//              afterwards L_ij = a_ij / sqrt(a_jj)
+//   inverse :  X~_ic -= a_ij / a_jj * X~_jc      (i > j, c <= j; row j of X~ is final)
+//              afterwards Linv_ic = X~_ic / sqrt(a_ii)
+// (reads and writes of a step touch disjoint entries, so no second barrier is needed; M barriers in all).
 __global__ __launch_bounds__(256) void k_chol_inv_lds(int M, const double2* __restrict__ Cr,
                                                       double2* __restrict__ Linv, const double* __restrict__ logw,
                                                       double* __restrict__ cconst, int* __restrict__ status) {
   __shared__ double2 a[64 * 64];
   __shared__ double2 x[64 * 64];
   __shared__ double piv[64];
+  // (row, column) of the row-major lower triangle of the trailing block per entry t: every step's triangle is a
+  // prefix of the largest one, so one table serves all steps (no per-entry square root)
+  __shared__ unsigned short tri_rc[63 * 64 / 2];
   const int k = blockIdx.x, tid = threadIdx.x;
   const double2* src = Cr + (long long)k * M * M;
   for (int e = tid; e < M * M; e += 256) {
@@ -405,6 +408,8 @@ __global__ __launch_bounds__(256) void k_chol_inv_lds(int M, const double2* __re
     a[r * 64 + c] = src[e];
     x[r * 64 + c] = make_double2(r == c ? 1.0 : 0.0, 0.0);
   }
+  for (int rr = tid >> 6; rr < 63; rr += 4)
+    for (int cc = tid & 63; cc <= rr; cc += 64) tri_rc[rr * (rr + 1) / 2 + cc] = (unsigned short)((rr << 8) | cc);
   __syncthreads();
   bool bad = false;
   for (int j = 0; j < M; ++j) {
@@ -417,15 +422,23 @@ __global__ __launch_bounds__(256) void k_chol_inv_lds(int M, const double2* __re
     const int n = M - j - 1;
     const int tri = n * (n + 1) / 2;
     for (int t = tid; t < tri; t += 256) {
-      // t -> (r, c) with r >= c in the trailing block, row-major over the lower triangle
-      int rr = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-      if ((rr + 1) * (rr + 2) / 2 <= t) ++rr;
-      if (rr * (rr + 1) / 2 > t) --rr;
-      const int cc = t - rr * (rr + 1) / 2;
-      const int r = j + 1 + rr, c = j + 1 + cc;
+      const unsigned v = tri_rc[t];  // t -> (r, c), r >= c, in the trailing block
+      const int r = j + 1 + (int)(v >> 8), c = j + 1 + (int)(v & 255u);
       const double2 arj = a[r * 64 + j], acj = a[c * 64 + j];
       const double2 pr = cmulc(arj, acj);
       a[r * 64 + c] = csub(a[r * 64 + c], make_double2(pr.x * inv, pr.y * inv));
+    }
+    // inverse step j in the same phase: it needs column j of the factor (final since step j - 1, not written by
+    // the update above) and row j of X~ (final since step j - 1), and writes only X~ rows below j
+    const int nr = M - j - 1, nc = j + 1;
+    const float rnc = 1.0f / (float)nc;  // t / nc through an fp32 reciprocal and one correction (t < 4096)
+    for (int t = tid; t < nr * nc; t += 256) {
+      int q = (int)((float)t * rnc);
+      q += (q + 1) * nc <= t ? 1 : 0;
+      q -= q * nc > t ? 1 : 0;
+      const int i = j + 1 + q, c = t - q * nc;
+      const double2 l = a[i * 64 + j];
+      x[i * 64 + c] = csub(x[i * 64 + c], cmul(make_double2(l.x * inv, l.y * inv), x[j * 64 + c]));
     }
     __syncthreads();
   }
@@ -434,16 +447,7 @@ __global__ __launch_bounds__(256) void k_chol_inv_lds(int M, const double2* __re
     return;
   }
   for (int i = tid; i < M; i += 256) piv[i] = sqrt(a[i * 64 + i].x);
-  for (int kk = 0; kk < M; ++kk) {
-    const double inv = 1.0 / a[kk * 64 + kk].x;
-    const int nr = M - kk - 1, nc = kk + 1;
-    for (int t = tid; t < nr * nc; t += 256) {
-      const int i = kk + 1 + t / nc, c = t % nc;
-      const double2 l = a[i * 64 + kk];
-      x[i * 64 + c] = csub(x[i * 64 + c], cmul(make_double2(l.x * inv, l.y * inv), x[kk * 64 + c]));
-    }
-    __syncthreads();
-  }
+  __syncthreads();
   double2* dst = Linv + (long long)k * M * M;
   for (int e = tid; e < M * M; e += 256) {
     const int r = e / M, c = e % M;
