@@ -10,9 +10,15 @@ __global__ __launch_bounds__(256) void k_merge_f64(long long B, int N, int K, in
                                                    double* __restrict__ om, double* __restrict__ os,
                                                    double* __restrict__ oa, double* __restrict__ pk,
                                                    const double* __restrict__ shift) {
-  const long long b = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (b >= B || L <= 0) return;
+  // One wave per row.  Its lanes first take one partial record each (the row's maximum, then the record weights
+  // e^{m_w - max}, staged in LDS: computed once per record instead of once per output element), then the output
+  // elements n = lane, lane + 64 (N <= 128 on the fused FP64 kernel), accumulated in registers over chunks of 64
+  // records.
+  __shared__ double wsc[4][64];
+  __shared__ long long wrec[4][64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const long long b = (long long)blockIdx.x * 4 + wv;
+  if (b >= B || L <= 0) return;  // wave-uniform
   const long long t = b / TS, ls = b % TS;
   const long long wa = (t * K) / L, wb = ((t + 1) * K - 1) / L;
   if (wa == wb) return;
@@ -20,23 +26,47 @@ __global__ __launch_bounds__(256) void k_merge_f64(long long B, int N, int K, in
     const long long tf = (w * L) / K;
     return (w * 2 + (t == tf ? 0 : 1)) * TS + ls;
   };
+  const int nrec = (int)(wb - wa + 1);
   double mx = QCE_NEG_INF;
-  for (long long w = wa; w <= wb; ++w) mx = fmax(mx, pm[rec_of(w)]);
-  double s = 0.0;
-  for (long long w = wa; w <= wb; ++w) {
-    const long long r = rec_of(w);
-    s += (pm[r] == QCE_NEG_INF) ? 0.0 : ps[r] * exp(pm[r] - mx);
-  }
-  const double psc = (pk && mx != QCE_NEG_INF) ? exp(mx - *shift) : 0.0;  // shifted packed output
-  for (int n = lane; n < N; n += 64) {
-    double re = 0.0, im = 0.0;
-    for (long long w = wa; w <= wb; ++w) {
-      const long long r = rec_of(w);
+  for (int q = lane; q < nrec; q += 64) mx = fmax(mx, pm[rec_of(wa + q)]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+  double s = 0.0, re0 = 0.0, im0 = 0.0, re1 = 0.0, im1 = 0.0;
+  const int n0 = lane, n1 = lane + 64;
+  for (int c0 = 0; c0 < nrec; c0 += 64) {
+    const int nc = nrec - c0 < 64 ? nrec - c0 : 64;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous chunk's LDS reads are done
+    __builtin_amdgcn_wave_barrier();
+    if (lane < nc) {
+      const long long r = rec_of(wa + c0 + lane);
       const double sc = (pm[r] == QCE_NEG_INF) ? 0.0 : exp(pm[r] - mx);
-      const double2 v = *reinterpret_cast<const double2*>(pa + r * 2 * N + 2 * n);
-      re = fma(v.x, sc, re);
-      im = fma(v.y, sc, im);
+      wsc[wv][lane] = sc;
+      wrec[wv][lane] = r;
+      s = fma(ps[r], sc, s);
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int q = 0; q < nc; ++q) {
+      const double sc = wsc[wv][q];
+      const double* rp = pa + wrec[wv][q] * 2 * N;
+      if (n0 < N) {
+        const double2 v = *reinterpret_cast<const double2*>(rp + 2 * n0);
+        re0 = fma(v.x, sc, re0);
+        im0 = fma(v.y, sc, im0);
+      }
+      if (n1 < N) {
+        const double2 v = *reinterpret_cast<const double2*>(rp + 2 * n1);
+        re1 = fma(v.x, sc, re1);
+        im1 = fma(v.y, sc, im1);
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o);
+  const double psc = (pk && mx != QCE_NEG_INF) ? exp(mx - *shift) : 0.0;  // shifted packed output
+  auto put = [&](int n, double re, double im) {
+    if (n >= N) return;
     if (h) {
       h[b * N + n] = make_double2(re / s, im / s);
     } else if (pk) {
@@ -44,7 +74,9 @@ __global__ __launch_bounds__(256) void k_merge_f64(long long B, int N, int K, in
     } else {
       *reinterpret_cast<double2*>(oa + b * 2 * N + 2 * n) = make_double2(re, im);
     }
-  }
+  };
+  put(n0, re0, im0);
+  put(n1, re1, im1);
   if (!h && lane == 0) {
     if (pk) {
       *reinterpret_cast<double2*>(pk + b * (2 * N + 2)) = make_double2(s * psc, 0.0);
