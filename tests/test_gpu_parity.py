@@ -458,6 +458,8 @@ def test_fourier_mfma_kernel_vs_lds_kernel(K, N, blocks, B, n_bits, mean, monkey
     (64, 64, (2, 32), 500, 2),      # pass 1 = n2 bit 4 + the n1 bit
     (48, 64, (4, 16), 400, 2),      # pass 1 = both n1 bits, j = 0
     (40, 64, (16, 4), 300, 1),      # n2 = 4: pass 1 on n1 with j != 0, pass 2 mixes both axes
+    (128, 64, None, 1, 3),          # one observation: a single ragged tile (descriptor-extent loads / stores)
+    (128, 256, (4, 64), 5, 2),      # five observations on the N = 256 kernel
 ])
 def test_fourier_chunk_kernel(K, N, blocks, B, n_bits, monkeypatch):
     """k_fft_chunk (zero-mean N = 128, 256: components split over the waves for lp / softmax, bins for the
