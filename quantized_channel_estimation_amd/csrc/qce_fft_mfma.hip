@@ -6,7 +6,16 @@
 // whole of the arithmetic (4 K N flops per estimate) and run here on v_mfma_f64_16x16x4_f64, so the
 // result keeps the FP64 accuracy of the reference (gmm_cplx_bussgang.py computes in complex128).
 //
-// Workgroup = 4 waves and TS = 4096 / N observations (64 for N <= 64): the tile of spectra (TS x N
+// Kernels (dispatch in launch_mfma_out; QCE_FFT_CHUNK=0 at prepare time keeps the round-2 pair):
+//   k_fft_wreg   zero-mean N = 64: persistent one-wave tiles, register transform (pass 1 / LDS exchange / pass 2)
+//   k_fft_chunk  zero-mean N = 128, 256: components split over the waves for lp / softmax, bins for the filter,
+//                two barriers per 128-component chunk; register transform for N = 256
+//   k_fft_wave   N = 16, 32 and models with means up to 64 (wave-local LDS transform)
+//   k_fft_mfma   N = 128, 256 with means (described next)
+// On gfx950 FP64 VALU instructions and FP64 MFMAs share the SIMD's issue budget (tools/probe/f64_pipe_probe.hip),
+// so the newer kernels are organised around fewer VALU instructions per MFMA.
+//
+// k_fft_mfma: workgroup = 4 waves and TS = 4096 / N observations (64 for N <= 64): the tile of spectra (TS x N
 // complex128 = 64 KB) sits in LDS for the transforms, two workgroups per CU.  Wave w owns 16 observations
 // (MFMA columns) and a range of NB = min(N, 64) bins, whose spectra (and |Y|^2) it keeps in registers through
 // the component loop: for N > 64 the KW = N / 64 waves of one observation group split the bins and add their
