@@ -67,7 +67,7 @@ def parse():
     ap.add_argument("--precision", default="f64", choices=["f64", "fast"],
                     help="dense 'all' arithmetic: f64 (the reference's complex128, default) or fast (fp16 split)")
     ap.add_argument("--chunks", type=int, default=0,
-                    help="K-shard pipeline chunks per batch (0 = sharding.default_chunks: 4, or 8 from 4 ranks on)")
+                    help="K-shard pipeline chunks per batch (0 = sharding.default_chunks: 2)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--collective", default="rs", choices=["rs", "ar"],
                     help="K-shard SUM collective: reduce-scatter (rank keeps its rows) or all-reduce")

@@ -121,9 +121,12 @@ def _packed_to_complex(rows):
 
 
 def default_chunks(world):
-    """Pipeline chunks per batch: 4, or 8 from four ranks on (the per-chunk collective shrinks with the rank
-    count, so more chunks keep the exposed last-chunk share small)."""
-    return 8 if world >= 4 else 4
+    """Pipeline chunks per batch: 2 at every rank count.  Measured per rank on one MI355X at the metric config
+    (tools/kshard_rank_sim.py, profiles/r03_kshard_rank_sim.txt): prepare + 1/2/4/8 partial launches take
+    1.49/1.51/1.66/1.92 ms at K/N = 16 (8 ranks), 2.62/2.68/2.84/3.10 at 32 and 4.99/5.07/5.18/5.46 at 64 -- every
+    extra chunk adds stream-K tails and merges -- while only the last chunk's reduce-scatter (1/c of ~0.3-0.5 ms)
+    is exposed, so two chunks give the smallest sum at N = 2, 4 and 8."""
+    return 2
 
 
 class ComponentShardEstimator:
