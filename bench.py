@@ -68,7 +68,10 @@ def parse():
                     help="dense 'all' arithmetic: f64 (the reference's complex128, default) or fast (fp16 split)")
     ap.add_argument("--chunks", type=int, default=0,
                     help="K-shard pipeline chunks per batch (0 = sharding.default_chunks: 2)")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--backend", default="native",
+                    help="K-shard collectives: native (libqce's own RCCL communicator, qce_kshard_*; torch.distributed "
+                         "over gloo only for the rendezvous, barriers and the timing MAX) or a torch.distributed "
+                         "backend (nccl = RCCL through torch, gloo) driving sharding.py's Python orchestration")
     ap.add_argument("--collective", default="rs", choices=["rs", "ar"],
                     help="K-shard SUM collective: reduce-scatter (rank keeps its rows) or all-reduce")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline budget per leg (0 = skip)")
@@ -181,6 +184,36 @@ def _cpu_model():
     return "unknown"
 
 
+def available_cpus():
+    """CPUs this process may actually use: the affinity mask, capped by a cgroup (v2 cpu.max / v1 cfs) CPU quota
+    when one is set.  Returns (count, basis)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0 and per > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    n, basis = aff, f"sched_getaffinity {aff}"
+    if quota is not None and quota < n:
+        n, basis = max(1, int(quota)), f"cgroup CPU quota {quota:g} (affinity {aff})"
+    # the host's declared CPU share per GPU job (the GPU box exports OMP_NUM_THREADS = its share)
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and 0 < int(share) < n:
+        n, basis = int(share), f"OMP_NUM_THREADS {share} = the job's CPU share (affinity {aff}, quota {quota})"
+    return n, basis + f"; nproc {os.cpu_count()}"
+
+
 def _pool_worker(args):
     """One Pool worker: the loop-faithful oracle on its shard, single-threaded BLAS (the reference's
     mp_gmm worker, Bussgang_GMM.py:16-17, one estimate_from_y per task incl. its prepare)."""
@@ -196,16 +229,18 @@ def _pool_worker(args):
 def cpu_baseline(cfg, means, covs, w, y, quantizer, budget_s):
     """The reference's CPU path timed on this host: the loop-faithful restatement
     (same per-(sample, component) op order as gmm_cplx_bussgang.py:223-228 incl. the redundant
-    C_k A_eff^H) (i) in one process, one BLAS thread, (ii) in a Pool of cpu_count()//2 single-thread
-    workers sharding the batch, as Bussgang_GMM.py:29-32 sizes its pool (capped at the 16 host cores
-    a one-GPU box grants), and (iii) the vectorised FP64 oracle ("optimised CPU", BLAS threads = the
-    pool size).  Bounded samples: the cost is linear in B (per-call prepare included)."""
+    C_k A_eff^H) (i) in one process, one BLAS thread, (ii) in a Pool of single-thread workers sharding the
+    batch, sized as Bussgang_GMM.py:29-32 sizes its pool (cpu_count()//2) from the CPUs this process can
+    actually use (affinity mask and cgroup quota, measured: available_cpus), and (iii) the vectorised FP64
+    oracle ("optimised CPU", BLAS threads = the pool size).  Bounded samples: the cost is linear in B
+    (per-call prepare included)."""
     import multiprocessing as mp
     from threadpoolctl import threadpool_limits
     from oracle import qce_oracle as O
     N, snr, nb, qt = cfg["N"], cfg["snr"], cfg["n_bits"], cfg["qtype"]
     nproc = os.cpu_count() or 1
-    npool = max(1, min(nproc // 2, 16))
+    avail, basis = available_cpus()
+    npool = max(1, avail // 2)
 
     def loop(n):
         t0 = time.perf_counter()
@@ -224,10 +259,14 @@ def cpu_baseline(cfg, means, covs, w, y, quantizer, budget_s):
     nper = int(max(2, min(y.shape[0] // npool, (budget_s - prep) / per)))
     tasks = [(means, covs, w, y[i * nper:(i + 1) * nper], snr, N, nb, qt, quantizer) for i in range(npool)]
     ctx = mp.get_context("fork")
-    with ctx.Pool(npool) as pool:
+    pool = ctx.Pool(npool)
+    try:
         t0 = time.perf_counter()
         pool.map(_pool_worker, tasks, chunksize=1)
         dtp = time.perf_counter() - t0
+        pool.close()  # workers exit on their own (Pool.__exit__ would terminate() them with SIGTERM)
+    finally:
+        pool.join()
     pooled = npool * nper / dtp
     # (iii) vectorised oracle
     with threadpool_limits(limits=npool):
@@ -236,10 +275,10 @@ def cpu_baseline(cfg, means, covs, w, y, quantizer, budget_s):
         O.estimate(means, covs, w, y[:nv], snr, N, None, "all", nb, qt, quantizer)
         dtv = time.perf_counter() - t0
     return dict(value=round(pooled, 2), unit="channel estimates/s", cores=npool, kind="port",
-                sample=f"Pool({npool}) of single-thread workers (Bussgang_GMM.py:29-32 sizing, capped at 16), "
+                sample=f"Pool({npool}) of single-thread workers (Bussgang_GMM.py:29-32 sizing: available CPUs // 2), "
                        f"{nper} observations each through oracle.estimate_loop (per-call prepare included), "
                        f"{dtp:.1f} s wall",
-                nproc=nproc, cpu_model=_cpu_model(), single_process=single,
+                nproc=nproc, cpus_available=avail, cpus_basis=basis, cpu_model=_cpu_model(), single_process=single,
                 vectorised=dict(value=round(nv / dtv, 2), cores=npool,
                                 sample=f"{nv} observations through oracle.estimate (vectorised FP64), {dtv:.2f} s"))
 
@@ -287,7 +326,7 @@ def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
         achieved = useful / (kern_ms * 1e-3) / 1e12
         frac = achieved / FP64_MFMA_PEAK_TFLOPS
         assert frac <= 1.0, f"roofline frac {frac:.4f} > 1: the useful-work count or the kernel timing is wrong"
-        kernel = "k_est_all_f64 (+k_merge_f64)" if N <= 128 else "k_lp_f64 + k_select + k_wsum_f64"
+        kernel = "k_est_all_f64 (+k_merge_f64)" if N <= 128 else "k_lp_f64 + k_wsum_weights + k_wsum_f64"
         line = dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
                     frac=round(frac, 4), traffic=traffic, kernel=kernel, peak_dtype="fp64 MFMA (dense)",
                     kernel_ms=round(kern_ms, 4), useful_flops_per_estimate_component=useful_per,
@@ -410,11 +449,12 @@ def main():
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(cfg, means, covs, w, y, quantizer, args.cpu_seconds)
     torch.cuda.set_device(local)
+    native = args.backend == "native"
     if world > 1:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(args.backend)
+        else:  # native: the data path runs on libqce's RCCL communicator; gloo carries the control traffic
+            dist.init_process_group("gloo" if native else args.backend)
         world = dist.get_world_size()
     kshard = args.shard == "k" and world > 1
     qkind = {"uniform": _lib.QUANT_UNIFORM, "lloyd": _lib.QUANT_LLOYD}[cfg["qtype"]]
@@ -443,6 +483,17 @@ def main():
             if ev is not None:
                 ev[0][1].record(stream)
             return None, out
+    elif native:
+        from quantized_channel_estimation_amd.sharding import make_comm
+        comm = make_comm(rank, world, local, kind="rccl")
+        shard = ComponentShardEstimator(means, covs, w, rank, world, device=local, precision=args.precision,
+                                        comm=comm)
+        dm = shard.dev
+
+        def step(ev=None):
+            # the library's step: prepare + shift MAX, chunked partials + RCCL reduce-scatters, flag MAX; no host sync
+            shard.prepare(None, cfg["snr"], cfg["n_bits"], *qargs, stream=sptr)
+            return shard.estimate(yd, chunks=args.chunks or None, scatter=args.collective == "rs", sync=False)
     else:
         shard = ComponentShardEstimator(means, covs, w, rank, world, device=local, precision=args.precision)
         dm = shard.dev
@@ -475,24 +526,34 @@ def main():
         # K-shard: the natural sync point of a run of steps -- Cholesky failures raise, flagged rows are recombined
         return shard.finish() if kshard else res
 
+    res = None
     for _ in range(args.warmup):
         res = step()
-    finish(res)
+    if args.warmup > 0:
+        finish(res)
     barrier()
-    if kshard:
+    if kshard and native:
+        shard.native.timing(True)  # HIP events around every partial launch on the compute stream (qce_kshard_timing)
+        events = None
+    elif kshard:
         events = [[] for _ in range(args.steps)]  # filled per chunk by the timed partial launches
     else:
         events = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
                   for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        res = step(events[i])
+        res = step(None if events is None else events[i])
     res = finish(res)
     barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([sum(a.elapsed_time(b) for a, b in evs) for evs in events]))
+    if events is None:
+        tot, _ = shard.native.kernel_ms()
+        shard.native.timing(False)
+        kern_ms = tot / args.steps
+    else:
+        kern_ms = float(np.mean([sum(a.elapsed_time(b) for a, b in evs) for evs in events]))
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cpu" if native else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
     ms_per_step = elapsed / args.steps * 1e3
@@ -559,7 +620,9 @@ def main():
                                    f"{'' if args.shard == 'k' else '/GPU'} prepare-per-step",
                        "K": K, "N": N, "B": B, "shard": args.shard,
                        "parallelism": f"{'kshard' if args.shard == 'k' else 'batch'}{world}",
-                       "chunks": (args.chunks or default_chunks(world)) if kshard else None},
+                       "chunks": (args.chunks or default_chunks(world)) if kshard else None,
+                       "collectives": ("libqce RCCL communicator (qce_kshard_*)" if native else
+                                       f"torch.distributed {args.backend}") if kshard else None},
             "mse": mse,
             "parity": parity,
             "roofline": roofline,
@@ -567,6 +630,10 @@ def main():
         }
         line.update(extras)
         print(json.dumps(line), flush=True)
+    if kshard and native:  # tear the communicator down while every rank is still here
+        torch.cuda.synchronize(dev)
+        shard.native.close()
+        comm.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -35,6 +35,7 @@ typedef struct qce_model qce_model;
 #define QCE_ENOTIMPL 3 /* configuration the kernels do not cover          -> NotImplementedError */
 #define QCE_EHIP 4     /* HIP runtime failure                              -> RuntimeError        */
 #define QCE_ESTATE 5   /* call order (estimate before prepare)             -> RuntimeError        */
+#define QCE_ECOMM 6    /* communicator / collective failure (RCCL or host transport) -> RuntimeError */
 
 /* estimate modes (gmm_cplx_bussgang.py:197-242) */
 #define QCE_MODE_ALL 0  /* 'all': sum of all responsibility-weighted LMMSE estimates   (:220-228) */
@@ -234,6 +235,78 @@ int qce_rate_mf(const double* h_est, const double* h, int64_t B, int N, const do
 
 /* Device synchronisation of the model's stream (for timing and for QCE_IO_DEVICE callers). */
 int qce_synchronize(qce_model* model);
+
+/* ---------------------------------------------------------------------------------------------------------------
+ * K-shard estimation over a communicator.  Replaces the reference's only parallelism,
+ * a process pool over SNR points (Bussgang_GMM.py:29-32, :287), by one process per GPU, each holding a contiguous
+ * slice of the mixture's components (qce_kshard_slice), with the collectives issued by the library itself:
+ * RCCL (ncclAllReduce / ncclReduceScatter / ncclAllGather over xGMI) or a caller-supplied host transport.
+ * ------------------------------------------------------------------------------------------------------------- */
+typedef struct qce_comm qce_comm;
+typedef struct qce_kshard qce_kshard;
+
+#define QCE_COMM_ID_BYTES 128 /* ncclUniqueId */
+#define QCE_COMM_RCCL 0
+#define QCE_COMM_HOST 1
+
+/* collective ops of a host transport; all data are doubles */
+#define QCE_COLL_ALLREDUCE_SUM 0 /* recv[i] = sum_r send_r[i], count elements                          */
+#define QCE_COLL_ALLREDUCE_MAX 1 /* recv[i] = max_r send_r[i], count elements                          */
+#define QCE_COLL_REDUCE_SCATTER_SUM 2 /* send: world * count, recv[i] = sum_r send_r[rank * count + i]  */
+#define QCE_COLL_ALLGATHER 3     /* send: count, recv[r * count + i] = send_r[i]                      */
+
+/* A host transport (MPI, gloo, ...): called synchronously with host buffers (the library has synchronised the
+ * stream and staged the device data); returns 0 on success. */
+typedef int (*qce_host_collective)(void* user, int op, const double* send, double* recv, int64_t count);
+
+/* ncclGetUniqueId: called on one rank, the QCE_COMM_ID_BYTES bytes are then shared with every rank. */
+int qce_comm_unique_id(void* id_out);
+/* ncclCommInitRank on `device` (collective over the `world` ranks). */
+int qce_comm_init(const void* unique_id, int rank, int world, int device, qce_comm** out);
+/* A communicator whose collectives go through the caller's host transport `fn` (`user` passed through). */
+int qce_comm_init_host(int rank, int world, int device, qce_host_collective fn, void* user, qce_comm** out);
+int qce_comm_destroy(qce_comm* comm);
+int qce_comm_info(qce_comm* comm, int* rank, int* world, int* device, int* kind);
+
+/* Components [lo, hi) of rank `rank` in the balanced contiguous split of K over `world` ranks (K >= world). */
+int qce_kshard_slice(int K, int world, int rank, int* lo, int* hi);
+/* Rows of h_out a rank receives from qce_kshard_estimate: per pipeline chunk the global row range
+ * [ranges[2i], ranges[2i+1]) (concatenated in h_out in this order); scatter = 0: every rank gets all B rows.
+ * `cap` = number of ranges the array holds; *n = ranges written.  Selective modes use chunks = 1. */
+int qce_kshard_rows(int64_t B, int chunks, int world, int rank, int scatter, int64_t* ranges, int cap, int* n);
+
+/* A K-shard estimator: `shard` holds components qce_kshard_slice(K_total, world, rank) of the mixture (a model
+ * created from that slice), `comm` its communicator.  Neither is owned. */
+int qce_kshard_create(qce_model* shard, qce_comm* comm, int K_total, qce_kshard** out);
+int qce_kshard_destroy(qce_kshard* ks);
+/* Per-SNR prepare of the shard (qce_prepare) and the shared shift M* = max over ALL components of
+ * c_k = -M log(pi) + 2 log det P_k + log w_k (>= every lp: the quad form is >= 0), one MAX all-reduce on `stream`
+ * that also carries every rank's Cholesky status (+inf).  No host synchronisation (host transports aside). */
+int qce_kshard_prepare(qce_kshard* ks, const double* A, int M, double snr_db, double n_bits, int quant_kind,
+                       const double* thresholds, const double* labels, int n_levels, void* stream);
+/* One estimate step over y (B, M) c128 in device memory (the same y on every rank).
+ * QCE_MODE_ALL (gmm_cplx_bussgang.py:220-228): per chunk the shard's shifted FP64 partial rows
+ * [s e^{m-M*}, 0, acc e^{m-M*}] (qce_estimate_partial_shifted) and one SUM collective of them on the library's
+ * communication stream (reduce-scatter, scatter != 0, or all-reduce), overlapped with the next chunk's kernel;
+ * h = acc / s.  QCE_MODE_TOPN / QCE_MODE_CUMP (:197-219, :229-242): n == 1 all-gathers each shard's (max lp, index)
+ * and the owner of the first global maximum contributes W_j y + b_j; otherwise the shards' lp are all-gathered,
+ * every rank selects the same components (k_select on the full lp) and the shards' weighted filter sums are
+ * summed (one chunk).  h_out: device memory, the rows qce_kshard_rows names.  A 2-double MAX of the step's flag
+ * word [rows whose shifted sum underflowed, Cholesky failure on any rank] closes the step; nothing is read on the
+ * host until qce_kshard_finish.  y and h_out must stay valid until then.  The caller's `stream` is ordered after
+ * the step's collectives. */
+int qce_kshard_estimate(qce_kshard* ks, const double* y, int64_t B, int mode, double mode_param, int chunks,
+                        int scatter, double* h_out, void* stream);
+/* The caller's sync point: reads the flag words (one host synchronisation).  QCE_ECHOL with the reference's
+ * message (gmm_cplx_bussgang.py:43-46) if a Cholesky factorisation failed on any rank -- on every rank; rows of
+ * the last step whose shifted sum underflowed are recombined exactly (collective: per-row MAX of the shards'
+ * running maxima, then the SUM); QCE_ESTATE if an earlier, already superseded step had such rows. */
+int qce_kshard_finish(qce_kshard* ks, void* stream);
+/* Kernel timing of the shard's estimate launches (HIP events around each partial / lp launch on the compute
+ * stream): enable != 0 starts recording (clears earlier records); qce_kshard_kernel_ms synchronises on the
+ * recorded events, returns their summed duration and count, and clears them. */
+int qce_kshard_timing(qce_kshard* ks, int enable);
+int qce_kshard_kernel_ms(qce_kshard* ks, double* total_ms, int* launches);
 
 #ifdef __cplusplus
 }

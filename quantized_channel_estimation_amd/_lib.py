@@ -11,13 +11,16 @@ import numpy as np
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("QCE_LIB") or os.path.join(_PKG, "libqce.so")  # QCE_LIB: diagnostic builds only
 
-QCE_OK, QCE_EARG, QCE_ECHOL, QCE_ENOTIMPL, QCE_EHIP, QCE_ESTATE = range(6)
+QCE_OK, QCE_EARG, QCE_ECHOL, QCE_ENOTIMPL, QCE_EHIP, QCE_ESTATE, QCE_ECOMM = range(7)
 MODE_ALL, MODE_TOPN, MODE_CUMP = 0, 1, 2
 OPT_BETA_FIRST = 1
 OPT_PRECISION = 2
 PRECISION_F64, PRECISION_FAST = 0, 1
 QUANT_UNIFORM, QUANT_LLOYD, QUANT_OTHER = 0, 1, 2
 IO_HOST, IO_DEVICE = 0, 1
+COMM_ID_BYTES = 128
+COMM_RCCL, COMM_HOST = 0, 1
+COLL_ALLREDUCE_SUM, COLL_ALLREDUCE_MAX, COLL_REDUCE_SCATTER_SUM, COLL_ALLGATHER = range(4)
 
 # The reference's message for a non-positive-definite Cr_k (gmm_cplx_bussgang.py:33-37, raised at :43-46); the
 # library returns the same text with QCE_ECHOL (csrc/qce_capi.hip check_status), the K-shard path raises it from
@@ -74,7 +77,30 @@ SIGNATURES = {
                                     ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int, _vp]),
     "qce_model_structure": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                            ctypes.POINTER(ctypes.c_int)]),
+    # K-shard over a communicator (csrc/qce_kshard.hip)
+    "qce_comm_unique_id": (ctypes.c_int, [_vp]),
+    "qce_comm_init": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "qce_comm_init_host": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp, ctypes.POINTER(_vp)]),
+    "qce_comm_destroy": (ctypes.c_int, [_vp]),
+    "qce_comm_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                     ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
+    "qce_kshard_slice": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                        ctypes.POINTER(ctypes.c_int)]),
+    "qce_kshard_rows": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,
+                                       ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
+    "qce_kshard_create": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.POINTER(_vp)]),
+    "qce_kshard_destroy": (ctypes.c_int, [_vp]),
+    "qce_kshard_prepare": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int, _vp,
+                                          _vp, ctypes.c_int, _vp]),
+    "qce_kshard_estimate": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                           ctypes.c_int, _vp, _vp]),
+    "qce_kshard_finish": (ctypes.c_int, [_vp, _vp]),
+    "qce_kshard_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "qce_kshard_kernel_ms": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
 }
+
+# qce_host_collective: int (*)(void* user, int op, const double* send, double* recv, int64_t count)
+HOST_COLLECTIVE = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.c_int, _c_dbl_p, _c_dbl_p, ctypes.c_int64)
 
 _lib = None
 
@@ -383,3 +409,154 @@ class DeviceModel:
         a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         check(load().qce_model_structure(self._h, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
         return a.value, b.value, c.value
+
+
+def kshard_slice(K, world, rank):
+    """Components [lo, hi) of `rank` in the library's balanced contiguous split (qce_kshard_slice)."""
+    lo, hi = ctypes.c_int(), ctypes.c_int()
+    check(load().qce_kshard_slice(int(K), int(world), int(rank), ctypes.byref(lo), ctypes.byref(hi)))
+    return lo.value, hi.value
+
+
+def kshard_rows(B, chunks, world, rank, scatter):
+    """Global row ranges [(r0, r1), ...] of the rows a rank's qce_kshard_estimate writes, in h_out order."""
+    cap = max(1, int(chunks)) + 1
+    arr = np.empty(2 * cap, dtype=np.int64)
+    n = ctypes.c_int()
+    check(load().qce_kshard_rows(int(B), int(chunks), int(world), int(rank), int(bool(scatter)), ptr(arr), cap,
+                                 ctypes.byref(n)))
+    return [(int(arr[2 * i]), int(arr[2 * i + 1])) for i in range(n.value)]
+
+
+class Comm:
+    """A libqce communicator (qce_comm): RCCL (``Comm(uid, rank, world, device)``, the uid from ``Comm.unique_id()``
+    on one rank) or a host transport (``Comm.host(rank, world, device, fn)`` with fn(op, send, recv) on numpy
+    float64 arrays, e.g. torch.distributed over gloo)."""
+
+    @staticmethod
+    def unique_id():
+        buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+        check(load().qce_comm_unique_id(ctypes.cast(buf, _vp)))
+        return buf.raw
+
+    def __init__(self, uid, rank, world, device=0):
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError(f"unique id must be {COMM_ID_BYTES} bytes")
+        buf = ctypes.create_string_buffer(bytes(uid), COMM_ID_BYTES)
+        h = _vp()
+        check(load().qce_comm_init(ctypes.cast(buf, _vp), int(rank), int(world), int(device), ctypes.byref(h)))
+        self._h, self._cb = h, None
+        self.rank, self.world, self.device, self.kind = int(rank), int(world), int(device), COMM_RCCL
+
+    @classmethod
+    def host(cls, rank, world, device, fn):
+        """fn(op, send, recv) -> None with send / recv numpy float64 views (QCE_COLL_* semantics, include/qce.h)."""
+        self = cls.__new__(cls)
+        world = int(world)
+
+        def tramp(_user, op, send, recv, count):
+            try:
+                ns = count * world if op == COLL_REDUCE_SCATTER_SUM else count
+                nr = count * world if op == COLL_ALLGATHER else count
+                fn(op, np.ctypeslib.as_array(send, shape=(ns,)), np.ctypeslib.as_array(recv, shape=(nr,)))
+                return 0
+            except Exception:  # pragma: no cover - surfaces as QCE_ECOMM
+                import traceback
+                traceback.print_exc()
+                return 1
+        self._cb = HOST_COLLECTIVE(tramp)
+        h = _vp()
+        check(load().qce_comm_init_host(int(rank), world, int(device), ctypes.cast(self._cb, _vp), None,
+                                        ctypes.byref(h)))
+        self._h = h
+        self.rank, self.world, self.device, self.kind = int(rank), world, int(device), COMM_HOST
+        return self
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().qce_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class KShard:
+    """qce_kshard: the K-shard estimator of one rank over a Comm; `model` is the DeviceModel of this rank's
+    components kshard_slice(K, world, rank)."""
+
+    def __init__(self, model, comm, K_total):
+        h = _vp()
+        check(load().qce_kshard_create(model.handle, comm.handle, int(K_total), ctypes.byref(h)))
+        self._h, self.model, self.comm, self.K = h, model, comm, int(K_total)
+        self._keep = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().qce_kshard_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def prepare(self, A, snr_db, n_bits, quant_kind=QUANT_UNIFORM, thresholds=None, labels=None, stream=None):
+        m = self.model
+        if A is None:
+            M, a = m.N, None
+        else:
+            a = np.ascontiguousarray(A, dtype=np.complex128)
+            if a.ndim != 2 or a.shape[1] != m.N:
+                raise ValueError(f"A must be (M, {m.N}), got {a.shape}")
+            M = a.shape[0]
+        thr = lab = None
+        nlev = 0
+        if labels is not None:
+            lab = np.ascontiguousarray(labels, dtype=np.float64)
+            thr = np.ascontiguousarray(thresholds, dtype=np.float64)
+            nlev = lab.size
+        check(load().qce_kshard_prepare(self._h, ptr(a), int(M), float(snr_db), float(n_bits), int(quant_kind),
+                                        ptr(thr), ptr(lab), int(nlev), stream))
+        m.M = M
+
+    def estimate(self, y, mode=MODE_ALL, param=0.0, chunks=2, scatter=True, out=None, stream=None):
+        """y (B, M) complex128 CUDA tensor (the same on every rank) -> (rows, h): h the estimates of the global rows
+        `rows` (a list of (r0, r1) ranges in h's row order).  Asynchronous on `stream`; finish() is the sync point."""
+        import torch
+        B = y.shape[0]
+        ch = int(chunks) if mode == MODE_ALL else 1
+        rows = kshard_rows(B, ch, self.comm.world, self.comm.rank, scatter)
+        n = sum(b - a for a, b in rows)
+        if out is None:
+            out = torch.empty((n, self.model.N), dtype=torch.complex128, device=y.device)
+        elif tuple(out.shape) != (n, self.model.N):
+            raise ValueError(f"out must be ({n}, {self.model.N})")
+        if y.shape[1] != self.model.M:
+            raise ValueError(f"y must have {self.model.M} columns, got {y.shape[1]}")
+        check(load().qce_kshard_estimate(self._h, ptr(y), int(B), int(mode), float(param), ch, int(bool(scatter)),
+                                         ptr(out), stream))
+        self._keep = (y, out)  # y and h must stay alive until finish()
+        return rows, out
+
+    def finish(self, stream=None):
+        try:
+            check(load().qce_kshard_finish(self._h, stream))
+        finally:
+            self._keep = None
+
+    def timing(self, enable):
+        check(load().qce_kshard_timing(self._h, int(bool(enable))))
+
+    def kernel_ms(self):
+        t, n = ctypes.c_double(), ctypes.c_int()
+        check(load().qce_kshard_kernel_ms(self._h, ctypes.byref(t), ctypes.byref(n)))
+        return t.value, n.value

@@ -1,0 +1,855 @@
+// K-shard estimation over a communicator (include/qce.h).
+//
+// The reference's only parallelism is a process pool over SNR points (Bussgang_GMM.py:29-32, :287); here one
+// SNR point's mixture is split over the GPUs of a node by components, one process per GPU, and the library issues
+// the collectives itself -- RCCL over xGMI (ncclAllReduce / ncclReduceScatter / ncclAllGather on device buffers) or
+// a caller-supplied host transport (the library stages through pinned host memory).
+//
+// 'all' mode (gmm_cplx_bussgang.py:220-228): every shard's estimate is written already scaled by the shared,
+// y-independent shift M* = max_k c_k (>= every lp_bk because the quad form is >= 0), so one SUM of the packed rows
+// [s e^{m - M*}, 0, acc e^{m - M*}] over the shards gives h = acc / s.  The batch is cut into chunks; chunk i's
+// reduce-scatter runs on the communication stream while chunk i+1's partial kernel runs on the compute stream.
+// Rows whose shifted sum leaves the normal FP64 range are counted on the device; one 2-double MAX per step agrees
+// on the flag word [flagged rows, Cholesky failure], read once at qce_kshard_finish, which recombines the flagged
+// step exactly with a per-row shift (MAX of the shards' running maxima, then the SUM).
+//
+// Selective modes (:197-219, :229-242): argmax all-gathers each shard's (max lp, index) and the owner of the first
+// global maximum contributes W_j y + b_j; top-n / cumulative-p all-gather the shards' lp so that every rank runs
+// the same FP64 selection (k_select) on the full row and contributes its own components' weighted filters.
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <rccl/rccl.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/qce.h"
+#include "qce_common.h"
+#include "qce_model.h"
+
+namespace {
+
+// a row whose shifted sum is below this is recombined exactly (sharding.py UNDERFLOW_S): above it every term that
+// matters is a normal double, so the shifted sums carry full FP64 precision
+constexpr double kUnderflowS = 1e-290;
+
+const char* kCholMessage =
+    "Fitting the mixture model failed because some components have ill-defined empirical covariance "
+    "(for instance caused by singleton or collapsed samples). Try to decrease the number of "
+    "components, or increase reg_covar.";
+
+#define KS_HIP(expr)                                                                               \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess)                                                                          \
+      return qce_set_error(QCE_EHIP, std::string(#expr) + " failed: " + hipGetErrorString(e_));    \
+  } while (0)
+
+#define KS_RC(expr)             \
+  do {                          \
+    int rc_ = (expr);           \
+    if (rc_ != QCE_OK) return rc_; \
+  } while (0)
+
+struct DevGuard {
+  int prev = -1;
+  explicit DevGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev && hipSetDevice(dev) != hipSuccess) (void)hipGetLastError();  // no sticky error left behind
+  }
+  ~DevGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+struct Chunk {
+  long long lo, hi;    // global rows of the chunk
+  long long npad;      // rows of the collective's send buffer (multiple of world under reduce-scatter)
+  long long r0, nv;    // this rank's rows of the chunk: [r0, r0 + nv)
+  long long pk_off;    // row offset of the chunk in the send buffer
+  long long rs_off;    // row offset in the receive buffer (reduce-scatter)
+  long long h_off;     // row offset in h_out
+};
+
+// sharding.chunk_bounds: with scatter every chunk but the last holds a multiple of `world` rows
+std::vector<Chunk> chunk_layout(long long B, int chunks, int world, int rank, bool scatter) {
+  std::vector<Chunk> out;
+  if (B <= 0) return out;
+  long long c = chunks < 1 ? 1 : chunks;
+  const long long cap = B / (world > 1 ? world : 1);
+  if (c > (cap > 1 ? cap : 1)) c = cap > 1 ? cap : 1;
+  long long step = (B + c - 1) / c;
+  if (scatter) step = (step + world - 1) / world * world;
+  long long pk = 0, rs = 0, ho = 0;
+  for (long long lo = 0; lo < B;) {
+    Chunk ch;
+    ch.lo = lo;
+    ch.hi = lo + step < B ? lo + step : B;
+    const long long n = ch.hi - ch.lo;
+    if (scatter) {
+      ch.npad = (n + world - 1) / world * world;
+      const long long q = ch.npad / world;
+      ch.r0 = ch.lo + rank * q;
+      const long long e = ch.r0 + q < ch.hi ? ch.r0 + q : ch.hi;
+      ch.nv = e > ch.r0 ? e - ch.r0 : 0;
+      ch.rs_off = rs;
+      rs += q;
+    } else {
+      ch.npad = n;
+      ch.r0 = ch.lo;
+      ch.nv = n;
+      ch.rs_off = 0;
+    }
+    ch.pk_off = pk;
+    pk += ch.npad;
+    ch.h_off = ho;
+    ho += ch.nv;
+    out.push_back(ch);
+    lo = ch.hi;
+  }
+  return out;
+}
+
+void slice_of(int K, int world, int rank, int* lo, int* hi) {
+  const int base = K / world, rem = K % world;
+  *lo = rank * base + (rank < rem ? rank : rem);
+  *hi = *lo + base + (rank < rem ? 1 : 0);
+}
+
+// ---------------------------------------------------------------------------------------------------------------
+// kernels (HBM-bound row passes; grid-stride, 256 threads)
+// ---------------------------------------------------------------------------------------------------------------
+unsigned grid_for(long long n) {
+  long long b = (n + 255) / 256;
+  return (unsigned)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
+}
+
+// h[r] = acc[r] / s[r] from packed rows [s, 0, acc (2N)]; rows with s below the normal range are counted
+__global__ __launch_bounds__(256) void k_ks_finalize(long long n, int N, const double* __restrict__ rows,
+                                                     double2* __restrict__ h, double thr, unsigned* __restrict__ cnt) {
+  const long long W = 2LL * N + 2;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n * N; i += (long long)gridDim.x * 256) {
+    const long long b = i / N, j = i % N;
+    const double* r = rows + b * W;
+    const double s = r[0];
+    const double2 a = *reinterpret_cast<const double2*>(r + 2 + 2 * j);
+    h[b * N + j] = make_double2(a.x / s, a.y / s);
+    if (j == 0 && s < thr) atomicAdd(cnt, 1u);
+  }
+}
+
+// fl = [flagged rows, Cholesky failure on this rank (its shift slot carries +inf after the MAX)]
+__global__ void k_ks_flags(const unsigned* __restrict__ cnt, const double* __restrict__ shift, int local_chol,
+                           double* __restrict__ fl) {
+  if (threadIdx.x == 0) {
+    fl[0] = cnt ? (double)*cnt : 0.0;
+    fl[1] = (local_chol || isinf(*shift) || isnan(*shift)) ? 1.0 : 0.0;
+  }
+}
+
+// earlier = max(earlier, fl): a superseded step's flags (every step before the last is accounted for)
+__global__ void k_ks_fold(double* __restrict__ earlier, const double* __restrict__ fl) {
+  if (threadIdx.x < 2) earlier[threadIdx.x] = fmax(earlier[threadIdx.x], fl[threadIdx.x]);
+}
+
+// [m, s, acc] partial -> packed rows scaled by a per-row shift mg (the exact recombination of flagged steps)
+__global__ __launch_bounds__(256) void k_ks_pack_rowshift(long long B, int N, const double* __restrict__ m,
+                                                          const double* __restrict__ s, const double* __restrict__ acc,
+                                                          const double* __restrict__ mg, double* __restrict__ pk) {
+  const long long W = 2LL * N + 2;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < B * W; i += (long long)gridDim.x * 256) {
+    const long long b = i / W, j = i % W;
+    const double sc = (m[b] == -__builtin_inf()) ? 0.0 : exp(m[b] - mg[b]);
+    const double v = j == 0 ? s[b] : (j == 1 ? 0.0 : acc[b * 2 * N + j - 2]);
+    pk[i] = v * sc;
+  }
+}
+
+// test hook of the exact recombination (QCE_KSHARD_SHIFT_BIAS): raise the agreed shift so rows leave the range
+__global__ void k_ks_add(double* __restrict__ v, double d) {
+  if (threadIdx.x == 0) v[0] += d;
+}
+
+// first maximum of each lp row (numpy argmax) as (value, index) doubles, one wave per row
+__global__ __launch_bounds__(256) void k_ks_row_argmax(long long B, int K, const double* __restrict__ lp,
+                                                       double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const long long b = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  double bv = -__builtin_inf();
+  int bi = 1 << 30;
+  for (int k = lane; k < K; k += 64) {
+    const double v = lp[b * K + k];
+    if (v > bv || bi == (1 << 30)) {
+      bv = v;
+      bi = k;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(bv, o);
+    const int oi = __shfl_xor(bi, o);
+    if (ov > bv || (ov == bv && oi < bi)) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  if (lane == 0) {
+    out[2 * b] = bv;
+    out[2 * b + 1] = (double)bi;
+  }
+}
+
+// global winner of the gathered (value, local index) pairs: larger value, ties to the lower rank (= lower global
+// index, the shards are contiguous); the owner's weight row is one-hot, every other rank's row is zero
+__global__ __launch_bounds__(256) void k_ks_argmax_weights(long long B, int world, int rank, int Kl,
+                                                           const double* __restrict__ g, double* __restrict__ w) {
+  for (long long b = (long long)blockIdx.x * 256 + threadIdx.x; b < B; b += (long long)gridDim.x * 256) {
+    double bv = -__builtin_inf();
+    int br = -1, bi = 0;
+    for (int r = 0; r < world; ++r) {
+      const double v = g[((long long)r * B + b) * 2];
+      if (br < 0 || v > bv) {
+        bv = v;
+        br = r;
+        bi = (int)g[((long long)r * B + b) * 2 + 1];
+      }
+    }
+    for (int k = 0; k < Kl; ++k) w[b * Kl + k] = (br == rank && k == bi) ? 1.0 : 0.0;
+  }
+}
+
+// lp (B x Kl) -> (B x Kmax), padded with -inf (equal all-gather counts)
+__global__ __launch_bounds__(256) void k_ks_pad(long long B, int Kl, int Kmax, const double* __restrict__ lp,
+                                                double* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < B * Kmax; i += (long long)gridDim.x * 256) {
+    const long long b = i / Kmax;
+    const int k = (int)(i % Kmax);
+    out[i] = k < Kl ? lp[b * Kl + k] : -__builtin_inf();
+  }
+}
+
+// gathered (world x B x Kmax) -> the full row-major lp (B x K) in global component order
+__global__ __launch_bounds__(256) void k_ks_assemble(long long B, int world, int K, int Kmax,
+                                                     const double* __restrict__ g, double* __restrict__ lp) {
+  const int base = K / world, rem = K % world;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < B * K; i += (long long)gridDim.x * 256) {
+    const long long b = i / K;
+    const int kg = (int)(i % K);
+    const int r = kg < rem * (base + 1) ? kg / (base + 1) : rem + (kg - rem * (base + 1)) / base;
+    const int lo = r * base + (r < rem ? r : rem);
+    lp[i] = g[((long long)r * B + b) * Kmax + (kg - lo)];
+  }
+}
+
+// w_loc (B x Kl) = w_full[:, lo:lo+Kl]
+__global__ __launch_bounds__(256) void k_ks_slice(long long B, int K, int lo, int Kl, const double* __restrict__ wf,
+                                                  double* __restrict__ wl) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < B * Kl; i += (long long)gridDim.x * 256) {
+    const long long b = i / Kl;
+    wl[i] = wf[b * K + lo + (int)(i % Kl)];
+  }
+}
+
+template <typename T>
+struct KBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc(&p, sizeof(T) * (count ? count : 1));
+    if (e == hipSuccess) n = count;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+}  // namespace
+
+struct qce_comm {
+  int rank = 0, world = 1, device = 0, kind = QCE_COMM_RCCL;
+  ncclComm_t nc = nullptr;
+  qce_host_collective fn = nullptr;
+  void* user = nullptr;
+  double *pin_send = nullptr, *pin_recv = nullptr;  // host transport staging
+  size_t pin_cap_send = 0, pin_cap_recv = 0;
+};
+
+struct qce_kshard {
+  qce_model* m = nullptr;  // not owned; never dereferenced by qce_kshard_destroy (the model may already be gone)
+  int device = 0;
+  qce_comm* c = nullptr;
+  int K = 0, lo = 0, hi = 0, Kmax = 0;
+  hipStream_t cs = nullptr;  // communication stream: the chunks' collectives and row finalisation
+  std::vector<hipEvent_t> ev_chunk;
+  hipEvent_t ev_done = nullptr;
+  KBuf<double> shift, fl, earlier, pk, rs;
+  KBuf<unsigned> cnt;
+  double* host_fl = nullptr;  // pinned: [fl0, fl1, earlier0, earlier1] of the last step
+  int local_chol = 0;         // this rank's library refused a call with the reference's Cholesky error
+  // the last step, kept for finish(): exact recombination of flagged rows
+  struct {
+    int valid = 0;
+    const double2* y = nullptr;
+    long long B = 0;
+    int chunks = 1, scatter = 1, mode = QCE_MODE_ALL;
+    double2* h = nullptr;
+    int stale = 0;  // a prepare ran after the step: its rows can no longer be recombined with the step's tables
+  } pending;
+  int any_pending_before = 0;  // a step was superseded before finish(): its flags went into `earlier`
+  // repair / selective-mode scratch
+  KBuf<double> rm, rsum, racc, mg, lp, lpad, gath, lpfull, wfull, wloc;
+  // kernel timing
+  int timing = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> tev;
+  size_t tev_used = 0;
+};
+
+namespace {
+
+int comm_error(const std::string& what, ncclResult_t r) {
+  return qce_set_error(QCE_ECOMM, what + " failed: " + ncclGetErrorString(r));
+}
+
+// one collective of doubles on stream st (see the QCE_COLL_* semantics in qce.h)
+int collective(qce_comm* c, int op, const double* send, double* recv, long long count, hipStream_t st) {
+  if (count <= 0) return QCE_OK;
+  if (c->kind == QCE_COMM_RCCL) {
+    ncclResult_t r;
+    switch (op) {
+      case QCE_COLL_ALLREDUCE_SUM: r = ncclAllReduce(send, recv, (size_t)count, ncclFloat64, ncclSum, c->nc, st); break;
+      case QCE_COLL_ALLREDUCE_MAX: r = ncclAllReduce(send, recv, (size_t)count, ncclFloat64, ncclMax, c->nc, st); break;
+      case QCE_COLL_REDUCE_SCATTER_SUM:
+        r = ncclReduceScatter(send, recv, (size_t)count, ncclFloat64, ncclSum, c->nc, st);
+        break;
+      case QCE_COLL_ALLGATHER: r = ncclAllGather(send, recv, (size_t)count, ncclFloat64, c->nc, st); break;
+      default: return qce_set_error(QCE_EARG, "unknown collective");
+    }
+    if (r != ncclSuccess) return comm_error("RCCL collective", r);
+    return QCE_OK;
+  }
+  // host transport: synchronise, stage through pinned memory, call, copy back
+  const long long ns = (op == QCE_COLL_REDUCE_SCATTER_SUM) ? count * c->world : count;
+  const long long nr = (op == QCE_COLL_ALLGATHER) ? count * c->world : count;
+  if ((size_t)ns > c->pin_cap_send) {
+    if (c->pin_send) (void)hipHostFree(c->pin_send);
+    c->pin_send = nullptr;
+    c->pin_cap_send = 0;
+    KS_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->pin_send), sizeof(double) * ns, hipHostMallocDefault));
+    c->pin_cap_send = (size_t)ns;
+  }
+  if ((size_t)nr > c->pin_cap_recv) {
+    if (c->pin_recv) (void)hipHostFree(c->pin_recv);
+    c->pin_recv = nullptr;
+    c->pin_cap_recv = 0;
+    KS_HIP(hipHostMalloc(reinterpret_cast<void**>(&c->pin_recv), sizeof(double) * nr, hipHostMallocDefault));
+    c->pin_cap_recv = (size_t)nr;
+  }
+  KS_HIP(hipMemcpyAsync(c->pin_send, send, sizeof(double) * ns, hipMemcpyDeviceToHost, st));
+  KS_HIP(hipStreamSynchronize(st));
+  if (c->fn(c->user, op, c->pin_send, c->pin_recv, count) != 0)
+    return qce_set_error(QCE_ECOMM, "host collective failed");
+  KS_HIP(hipMemcpyAsync(recv, c->pin_recv, sizeof(double) * nr, hipMemcpyHostToDevice, st));
+  KS_HIP(hipStreamSynchronize(st));
+  return QCE_OK;
+}
+
+hipStream_t ks_stream(qce_kshard* ks, void* stream) {
+  if (stream) return (hipStream_t)stream;
+  return ks->m->stream;
+}
+
+// device call of this rank that may report the prepare's deferred Cholesky status: recorded instead of returned,
+// so the rank still joins every collective of the step and all ranks raise together at finish()
+bool guarded(qce_kshard* ks, int rc, int* hard) {
+  if (rc == QCE_OK) return true;
+  if (rc == QCE_ECHOL || (rc == QCE_ESTATE && ks->local_chol)) {
+    ks->local_chol = 1;
+    return false;
+  }
+  *hard = rc;
+  return false;
+}
+
+int timed_begin(qce_kshard* ks, hipStream_t st) {
+  if (!ks->timing) return QCE_OK;
+  if (ks->tev_used == ks->tev.size()) {
+    hipEvent_t a, b;
+    KS_HIP(hipEventCreate(&a));
+    KS_HIP(hipEventCreate(&b));
+    ks->tev.emplace_back(a, b);
+  }
+  KS_HIP(hipEventRecord(ks->tev[ks->tev_used].first, st));
+  return QCE_OK;
+}
+int timed_end(qce_kshard* ks, hipStream_t st) {
+  if (!ks->timing) return QCE_OK;
+  KS_HIP(hipEventRecord(ks->tev[ks->tev_used].second, st));
+  ks->tev_used++;
+  return QCE_OK;
+}
+
+// the SUM collectives of a step's packed rows (pk, W doubles per row) per chunk on the communication stream, each
+// behind its own chunk's producer on `st`, and the rows' finalisation h = acc / s into h_out
+int reduce_chunks(qce_kshard* ks, const std::vector<Chunk>& L, bool scatter, int W, hipStream_t st, double2* h_out,
+                  bool count_flags, size_t chunk_index) {
+  qce_comm* c = ks->c;
+  const int N = ks->m->N;
+  const Chunk& ch = L[chunk_index];
+  hipEvent_t ev = ks->ev_chunk[chunk_index];
+  KS_HIP(hipEventRecord(ev, st));
+  KS_HIP(hipStreamWaitEvent(ks->cs, ev, 0));
+  double* send = ks->pk.p + ch.pk_off * W;
+  const double* rows;
+  if (scatter) {
+    const long long q = ch.npad / c->world;
+    double* recv = ks->rs.p + ch.rs_off * W;
+    KS_RC(collective(c, QCE_COLL_REDUCE_SCATTER_SUM, send, recv, q * W, ks->cs));
+    rows = recv;
+  } else {
+    KS_RC(collective(c, QCE_COLL_ALLREDUCE_SUM, send, send, ch.npad * W, ks->cs));
+    rows = send;
+  }
+  if (ch.nv > 0) {
+    hipLaunchKernelGGL(k_ks_finalize, dim3(grid_for(ch.nv * N)), dim3(256), 0, ks->cs, ch.nv, N, rows,
+                       h_out + ch.h_off * N, count_flags ? kUnderflowS : -1.0, ks->cnt.p);
+    KS_HIP(hipGetLastError());
+  }
+  return QCE_OK;
+}
+
+int ensure_events(qce_kshard* ks, size_t n) {
+  while (ks->ev_chunk.size() < n) {
+    hipEvent_t e;
+    KS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ks->ev_chunk.push_back(e);
+  }
+  return QCE_OK;
+}
+
+// close a step: flag word MAX, pinned copy of [fl, earlier], the caller's stream ordered behind the comm stream
+int close_step(qce_kshard* ks, hipStream_t st) {
+  hipLaunchKernelGGL(k_ks_flags, dim3(1), dim3(64), 0, ks->cs, ks->cnt.p, ks->shift.p, ks->local_chol, ks->fl.p);
+  KS_HIP(hipGetLastError());
+  KS_RC(collective(ks->c, QCE_COLL_ALLREDUCE_MAX, ks->fl.p, ks->fl.p, 2, ks->cs));
+  KS_HIP(hipMemcpyAsync(ks->host_fl, ks->fl.p, 2 * sizeof(double), hipMemcpyDeviceToHost, ks->cs));
+  KS_HIP(hipMemcpyAsync(ks->host_fl + 2, ks->earlier.p, 2 * sizeof(double), hipMemcpyDeviceToHost, ks->cs));
+  KS_HIP(hipEventRecord(ks->ev_done, ks->cs));
+  KS_HIP(hipStreamWaitEvent(st, ks->ev_done, 0));
+  return QCE_OK;
+}
+
+// 'all' mode: per chunk the shifted partial on st (or, for the exact recombination, the per-row-shift rows of a
+// whole-batch FP64 partial), its SUM collective on cs, the finalisation
+int step_all(qce_kshard* ks, const double2* y, long long B, int chunks, bool scatter, double2* h, hipStream_t st,
+             bool rowshift) {
+  qce_model* m = ks->m;
+  qce_comm* c = ks->c;
+  const int N = m->N, M = m->M, W = 2 * N + 2;
+  std::vector<Chunk> L = chunk_layout(B, chunks, c->world, c->rank, scatter);
+  long long pk_rows = 0, rs_rows = 0;
+  for (const Chunk& ch : L) {
+    pk_rows += ch.npad;
+    if (scatter) rs_rows += ch.npad / c->world;
+  }
+  KS_HIP(ks->pk.ensure((size_t)pk_rows * W));
+  if (scatter) KS_HIP(ks->rs.ensure((size_t)rs_rows * W));
+  KS_RC(ensure_events(ks, L.size()));
+  int hard = QCE_OK;
+  if (rowshift) {
+    // exact recombination: m (running max), s, acc of this shard for the whole batch; mg = MAX over shards of m
+    KS_HIP(ks->rm.ensure((size_t)B));
+    KS_HIP(ks->rsum.ensure((size_t)B));
+    KS_HIP(ks->racc.ensure((size_t)B * 2 * N));
+    KS_HIP(ks->mg.ensure((size_t)B));
+    if (!guarded(ks, qce_estimate_partial_f64(m, reinterpret_cast<const double*>(y), B, ks->rm.p, ks->rsum.p,
+                                              ks->racc.p, QCE_IO_DEVICE, st), &hard)) {
+      if (hard) return hard;
+      KS_HIP(hipMemsetAsync(ks->rm.p, 0xff, sizeof(double) * B, st));  // NaN rows; the Cholesky flag raises first
+    }
+    KS_HIP(hipMemcpyAsync(ks->mg.p, ks->rm.p, sizeof(double) * B, hipMemcpyDeviceToDevice, st));
+    KS_RC(collective(c, QCE_COLL_ALLREDUCE_MAX, ks->mg.p, ks->mg.p, B, st));
+  }
+  for (size_t i = 0; i < L.size(); ++i) {
+    const Chunk& ch = L[i];
+    const long long n = ch.hi - ch.lo;
+    double* pk = ks->pk.p + ch.pk_off * W;
+    if (ch.npad > n) KS_HIP(hipMemsetAsync(pk + n * W, 0, sizeof(double) * (ch.npad - n) * W, st));
+    if (rowshift) {
+      hipLaunchKernelGGL(k_ks_pack_rowshift, dim3(grid_for(n * W)), dim3(256), 0, st, n, N, ks->rm.p + ch.lo,
+                         ks->rsum.p + ch.lo, ks->racc.p + ch.lo * 2 * N, ks->mg.p + ch.lo, pk);
+      KS_HIP(hipGetLastError());
+    } else {
+      bool ok = false;
+      if (!ks->local_chol) {
+        KS_RC(timed_begin(ks, st));
+        ok = guarded(ks, qce_estimate_partial_shifted(m, reinterpret_cast<const double*>(y + ch.lo * M), n,
+                                                      ks->shift.p, pk, QCE_IO_DEVICE, st), &hard);
+        if (hard) return hard;
+        KS_RC(timed_end(ks, st));
+      }
+      if (!ok) KS_HIP(hipMemsetAsync(pk, 0, sizeof(double) * n * W, st));
+    }
+    KS_RC(reduce_chunks(ks, L, scatter, W, st, h, !rowshift, i));
+  }
+  return QCE_OK;
+}
+
+// selective modes: global selection from the shards' lp, this shard's weighted filter sum, one SUM collective
+int step_select(qce_kshard* ks, const double2* y, long long B, int mode, double param, bool scatter, double2* h,
+                hipStream_t st) {
+  qce_model* m = ks->m;
+  qce_comm* c = ks->c;
+  const int N = m->N, Kl = m->K, W = 2 * N;
+  int kmode, nsel = 0;
+  double p = 0.0;
+  if (mode == QCE_MODE_TOPN) {
+    if (param < 1.0 || param != floor(param)) return qce_set_error(QCE_EARG, "top-n needs an integer n >= 1");
+    nsel = param > 1e9 ? 1000000000 : (int)param;
+    kmode = nsel == 1 ? 3 : 1;
+  } else if (mode == QCE_MODE_CUMP) {
+    kmode = 2;
+    p = param;
+  } else {
+    return qce_set_error(QCE_EARG, "unknown mode");
+  }
+  if (kmode != 3 && ks->K > 256) return qce_set_error(QCE_ENOTIMPL, "K-shard top-n / cumulative-p support K <= 256");
+  std::vector<Chunk> L = chunk_layout(B, 1, c->world, c->rank, scatter);
+  KS_RC(ensure_events(ks, 1));
+  const long long npad = L[0].npad;
+  KS_HIP(ks->lp.ensure((size_t)B * Kl));
+  KS_HIP(ks->wloc.ensure((size_t)B * Kl));
+  KS_HIP(ks->pk.ensure((size_t)npad * W));
+  if (scatter) KS_HIP(ks->rs.ensure((size_t)(npad / c->world) * W));
+  int hard = QCE_OK;
+  bool ok = false;
+  if (!ks->local_chol) {
+    KS_RC(timed_begin(ks, st));
+    ok = guarded(ks, qce_log_prob(m, reinterpret_cast<const double*>(y), B, ks->lp.p, nullptr, nullptr, QCE_IO_DEVICE,
+                                  st), &hard);
+    if (hard) return hard;
+    KS_RC(timed_end(ks, st));
+  }
+  if (!ok) KS_HIP(hipMemsetAsync(ks->lp.p, 0, sizeof(double) * B * Kl, st));
+  if (kmode == 3) {
+    // argmax: (max lp, local index) per row and shard -> the owner of the first global maximum
+    KS_HIP(ks->lpad.ensure((size_t)B * 2));
+    KS_HIP(ks->gath.ensure((size_t)B * 2 * c->world));
+    hipLaunchKernelGGL(k_ks_row_argmax, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, Kl, ks->lp.p, ks->lpad.p);
+    KS_HIP(hipGetLastError());
+    KS_RC(collective(c, QCE_COLL_ALLGATHER, ks->lpad.p, ks->gath.p, B * 2, st));
+    hipLaunchKernelGGL(k_ks_argmax_weights, dim3(grid_for(B)), dim3(256), 0, st, B, c->world, c->rank, Kl,
+                       ks->gath.p, ks->wloc.p);
+    KS_HIP(hipGetLastError());
+  } else {
+    const int K = ks->K, Kmax = ks->Kmax;
+    KS_HIP(ks->lpad.ensure((size_t)B * Kmax));
+    KS_HIP(ks->gath.ensure((size_t)B * Kmax * c->world));
+    KS_HIP(ks->lpfull.ensure((size_t)B * K));
+    KS_HIP(ks->wfull.ensure((size_t)B * K));
+    hipLaunchKernelGGL(k_ks_pad, dim3(grid_for(B * Kmax)), dim3(256), 0, st, B, Kl, Kmax, ks->lp.p, ks->lpad.p);
+    KS_HIP(hipGetLastError());
+    KS_RC(collective(c, QCE_COLL_ALLGATHER, ks->lpad.p, ks->gath.p, B * Kmax, st));
+    hipLaunchKernelGGL(k_ks_assemble, dim3(grid_for(B * K)), dim3(256), 0, st, B, c->world, K, Kmax, ks->gath.p,
+                       ks->lpfull.p);
+    KS_HIP(hipGetLastError());
+    // the same FP64 selection on every rank (gmm_cplx_bussgang.py:213, :235-236)
+    KS_HIP(qce_launch_select(B, K, ks->lpfull.p, kmode, nsel, p, nullptr, nullptr, nullptr, st, ks->wfull.p));
+    hipLaunchKernelGGL(k_ks_slice, dim3(grid_for(B * Kl)), dim3(256), 0, st, B, K, ks->lo, Kl, ks->wfull.p,
+                       ks->wloc.p);
+    KS_HIP(hipGetLastError());
+  }
+  // this shard's share of sum_k w_bk (W_k y_b + b_k), written straight into the collective's rows (a row of 2N
+  // doubles is one c128 row of h)
+  if (npad > B) KS_HIP(hipMemsetAsync(ks->pk.p + B * W, 0, sizeof(double) * (npad - B) * W, st));
+  ok = false;
+  if (!ks->local_chol) {
+    ok = guarded(ks, qce_weighted_estimate(m, y, B, ks->wloc.p, reinterpret_cast<double2*>(ks->pk.p), st), &hard);
+    if (hard) return hard;
+  }
+  if (!ok) KS_HIP(hipMemsetAsync(ks->pk.p, 0, sizeof(double) * B * W, st));
+  // SUM over shards on the communication stream, rows straight into h_out
+  const Chunk& ch = L[0];
+  KS_HIP(hipEventRecord(ks->ev_chunk[0], st));
+  KS_HIP(hipStreamWaitEvent(ks->cs, ks->ev_chunk[0], 0));
+  if (scatter) {
+    const long long q = npad / c->world;
+    KS_RC(collective(c, QCE_COLL_REDUCE_SCATTER_SUM, ks->pk.p, ks->rs.p, q * W, ks->cs));
+    if (ch.nv > 0)
+      KS_HIP(hipMemcpyAsync(h, ks->rs.p, sizeof(double) * ch.nv * W, hipMemcpyDeviceToDevice, ks->cs));
+  } else {
+    KS_RC(collective(c, QCE_COLL_ALLREDUCE_SUM, ks->pk.p, reinterpret_cast<double*>(h), B * W, ks->cs));
+  }
+  return QCE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qce_comm_unique_id(void* id_out) {
+  if (!id_out) return qce_set_error(QCE_EARG, "null id");
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return comm_error("ncclGetUniqueId", r);
+  memcpy(id_out, &id, sizeof(id));
+  return QCE_OK;
+}
+
+int qce_comm_init(const void* unique_id, int rank, int world, int device, qce_comm** out) {
+  if (!unique_id || !out) return qce_set_error(QCE_EARG, "null argument");
+  *out = nullptr;
+  if (world < 1 || rank < 0 || rank >= world) return qce_set_error(QCE_EARG, "rank / world out of range");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+    return qce_set_error(QCE_EARG, "device index out of range");
+  DevGuard g(device);
+  ncclUniqueId id;
+  memcpy(&id, unique_id, sizeof(id));
+  qce_comm* c = new qce_comm();
+  c->rank = rank;
+  c->world = world;
+  c->device = device;
+  c->kind = QCE_COMM_RCCL;
+  ncclResult_t r = ncclCommInitRank(&c->nc, world, id, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return comm_error("ncclCommInitRank", r);
+  }
+  *out = c;
+  return QCE_OK;
+}
+
+int qce_comm_init_host(int rank, int world, int device, qce_host_collective fn, void* user, qce_comm** out) {
+  if (!fn || !out) return qce_set_error(QCE_EARG, "null argument");
+  *out = nullptr;
+  if (world < 1 || rank < 0 || rank >= world) return qce_set_error(QCE_EARG, "rank / world out of range");
+  qce_comm* c = new qce_comm();
+  c->rank = rank;
+  c->world = world;
+  c->device = device;
+  c->kind = QCE_COMM_HOST;
+  c->fn = fn;
+  c->user = user;
+  *out = c;
+  return QCE_OK;
+}
+
+int qce_comm_destroy(qce_comm* c) {
+  if (!c) return QCE_OK;
+  DevGuard g(c->device);
+  if (c->nc) (void)ncclCommDestroy(c->nc);
+  if (c->pin_send) (void)hipHostFree(c->pin_send);
+  if (c->pin_recv) (void)hipHostFree(c->pin_recv);
+  delete c;
+  return QCE_OK;
+}
+
+int qce_comm_info(qce_comm* c, int* rank, int* world, int* device, int* kind) {
+  if (!c) return qce_set_error(QCE_EARG, "null comm");
+  if (rank) *rank = c->rank;
+  if (world) *world = c->world;
+  if (device) *device = c->device;
+  if (kind) *kind = c->kind;
+  return QCE_OK;
+}
+
+int qce_kshard_slice(int K, int world, int rank, int* lo, int* hi) {
+  if (!lo || !hi) return qce_set_error(QCE_EARG, "null argument");
+  if (world < 1 || rank < 0 || rank >= world || K < world)
+    return qce_set_error(QCE_EARG, "K-shard split needs K >= world and 0 <= rank < world");
+  slice_of(K, world, rank, lo, hi);
+  return QCE_OK;
+}
+
+int qce_kshard_rows(int64_t B, int chunks, int world, int rank, int scatter, int64_t* ranges, int cap, int* n) {
+  if (!ranges || !n || B < 0 || world < 1 || rank < 0 || rank >= world)
+    return qce_set_error(QCE_EARG, "bad arguments");
+  std::vector<Chunk> L = chunk_layout(B, chunks, world, rank, scatter != 0);
+  if ((int)L.size() > cap) return qce_set_error(QCE_EARG, "ranges array too small");
+  for (size_t i = 0; i < L.size(); ++i) {
+    ranges[2 * i] = L[i].r0;
+    ranges[2 * i + 1] = L[i].r0 + L[i].nv;
+  }
+  *n = (int)L.size();
+  return QCE_OK;
+}
+
+int qce_kshard_create(qce_model* shard, qce_comm* comm, int K_total, qce_kshard** out) {
+  if (!shard || !comm || !out) return qce_set_error(QCE_EARG, "null argument");
+  *out = nullptr;
+  if (K_total < comm->world) return qce_set_error(QCE_EARG, "K-shard split needs K >= world");
+  if (comm->kind == QCE_COMM_RCCL && comm->device != shard->device)
+    return qce_set_error(QCE_EARG, "model and communicator are on different devices");
+  int lo, hi;
+  slice_of(K_total, comm->world, comm->rank, &lo, &hi);
+  if (hi - lo != shard->K)
+    return qce_set_error(QCE_EARG, "the shard model must hold components [" + std::to_string(lo) + ", " +
+                                       std::to_string(hi) + ") of the balanced split (qce_kshard_slice)");
+  DevGuard g(shard->device);
+  qce_kshard* ks = new qce_kshard();
+  ks->m = shard;
+  ks->device = shard->device;
+  ks->c = comm;
+  ks->K = K_total;
+  ks->lo = lo;
+  ks->hi = hi;
+  ks->Kmax = (K_total + comm->world - 1) / comm->world;
+  hipError_t e = hipStreamCreateWithFlags(&ks->cs, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ks->ev_done, hipEventDisableTiming);
+  if (e == hipSuccess) e = ks->shift.ensure(1);
+  if (e == hipSuccess) e = ks->fl.ensure(2);
+  if (e == hipSuccess) e = ks->earlier.ensure(2);
+  if (e == hipSuccess) e = ks->cnt.ensure(1);
+  if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&ks->host_fl), 4 * sizeof(double), hipHostMallocDefault);
+  if (e == hipSuccess) e = hipMemset(ks->earlier.p, 0, 2 * sizeof(double));
+  if (e == hipSuccess) e = hipMemset(ks->fl.p, 0, 2 * sizeof(double));
+  if (e != hipSuccess) {
+    qce_kshard_destroy(ks);
+    return qce_set_error(QCE_EHIP, std::string("K-shard allocation failed: ") + hipGetErrorString(e));
+  }
+  *out = ks;
+  return QCE_OK;
+}
+
+int qce_kshard_destroy(qce_kshard* ks) {
+  if (!ks) return QCE_OK;
+  DevGuard g(ks->device);
+  if (ks->cs) (void)hipStreamSynchronize(ks->cs);
+  for (auto* b : {&ks->shift, &ks->fl, &ks->earlier, &ks->pk, &ks->rs, &ks->rm, &ks->rsum, &ks->racc, &ks->mg, &ks->lp,
+                  &ks->lpad, &ks->gath, &ks->lpfull, &ks->wfull, &ks->wloc})
+    b->release();
+  ks->cnt.release();
+  for (hipEvent_t e : ks->ev_chunk) (void)hipEventDestroy(e);
+  for (auto& pr : ks->tev) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
+  if (ks->ev_done) (void)hipEventDestroy(ks->ev_done);
+  if (ks->host_fl) (void)hipHostFree(ks->host_fl);
+  if (ks->cs) (void)hipStreamDestroy(ks->cs);
+  delete ks;
+  return QCE_OK;
+}
+
+int qce_kshard_prepare(qce_kshard* ks, const double* A, int M, double snr_db, double n_bits, int quant_kind,
+                       const double* thresholds, const double* labels, int n_levels, void* stream) {
+  if (!ks) return qce_set_error(QCE_EARG, "null K-shard");
+  DevGuard g(ks->device);
+  hipStream_t st = ks_stream(ks, stream);
+  ks->local_chol = 0;
+  if (ks->pending.valid) ks->pending.stale = 1;  // an exact recombination would need the replaced tables
+  KS_RC(qce_prepare(ks->m, A, M, snr_db, n_bits, quant_kind, thresholds, labels, n_levels, st));
+  int hard = QCE_OK;
+  if (!guarded(ks, qce_cconst_max(ks->m, ks->shift.p, QCE_IO_DEVICE, st), &hard)) {
+    if (hard) return hard;
+    const double inf = __builtin_inf();  // the failure rides the shift as the kernel would have written it
+    KS_HIP(hipMemcpyAsync(ks->shift.p, &inf, sizeof(double), hipMemcpyHostToDevice, st));
+    KS_HIP(hipStreamSynchronize(st));
+  }
+  KS_RC(collective(ks->c, QCE_COLL_ALLREDUCE_MAX, ks->shift.p, ks->shift.p, 1, st));
+  if (const char* b = getenv("QCE_KSHARD_SHIFT_BIAS")) {  // tests only: force the underflow path
+    hipLaunchKernelGGL(k_ks_add, dim3(1), dim3(64), 0, st, ks->shift.p, atof(b));
+    KS_HIP(hipGetLastError());
+  }
+  return QCE_OK;
+}
+
+int qce_kshard_estimate(qce_kshard* ks, const double* y, int64_t B, int mode, double mode_param, int chunks,
+                        int scatter, double* h_out, void* stream) {
+  if (!ks) return qce_set_error(QCE_EARG, "null K-shard");
+  if (B < 0 || (B > 0 && (!y || !h_out))) return qce_set_error(QCE_EARG, "bad y / h_out");
+  if (!ks->m->prepared && !ks->local_chol) return qce_set_error(QCE_ESTATE, "qce_kshard_prepare has not been called");
+  DevGuard g(ks->device);
+  hipStream_t st = ks_stream(ks, stream);
+  // a step superseded before finish(): its flags fold into the running `earlier` word
+  if (ks->pending.valid) {
+    hipLaunchKernelGGL(k_ks_fold, dim3(1), dim3(64), 0, ks->cs, ks->earlier.p, ks->fl.p);
+    KS_HIP(hipGetLastError());
+    ks->any_pending_before = 1;
+  }
+  KS_HIP(hipMemsetAsync(ks->cnt.p, 0, sizeof(unsigned), ks->cs));
+  const double2* yd = reinterpret_cast<const double2*>(y);
+  double2* hd = reinterpret_cast<double2*>(h_out);
+  if (B > 0) {
+    if (mode == QCE_MODE_ALL) {
+      KS_RC(step_all(ks, yd, B, chunks, scatter != 0, hd, st, false));
+    } else {
+      KS_RC(step_select(ks, yd, B, mode, mode_param, scatter != 0, hd, st));
+    }
+  }
+  KS_RC(close_step(ks, st));
+  ks->pending.valid = 1;
+  ks->pending.y = yd;
+  ks->pending.B = B;
+  ks->pending.chunks = mode == QCE_MODE_ALL ? chunks : 1;
+  ks->pending.scatter = scatter;
+  ks->pending.mode = mode;
+  ks->pending.h = hd;
+  ks->pending.stale = 0;
+  return QCE_OK;
+}
+
+int qce_kshard_finish(qce_kshard* ks, void* stream) {
+  if (!ks) return qce_set_error(QCE_EARG, "null K-shard");
+  if (!ks->pending.valid) return QCE_OK;
+  DevGuard g(ks->device);
+  hipStream_t st = ks_stream(ks, stream);
+  KS_HIP(hipEventSynchronize(ks->ev_done));
+  const double f0 = ks->host_fl[0], f1 = ks->host_fl[1], e0 = ks->host_fl[2], e1 = ks->host_fl[3];
+  auto pend = ks->pending;
+  ks->pending.valid = 0;
+  ks->any_pending_before = 0;
+  KS_HIP(hipMemsetAsync(ks->earlier.p, 0, 2 * sizeof(double), ks->cs));
+  if (f1 > 0.0 || e1 > 0.0) return qce_set_error(QCE_ECHOL, kCholMessage);
+  if (e0 > 0.0)
+    return qce_set_error(QCE_ESTATE, "an earlier K-shard estimate had rows whose shifted sum underflowed; call "
+                                     "qce_kshard_finish after each such step to have them recombined");
+  if (f0 > 0.0 && pend.mode == QCE_MODE_ALL && pend.stale)
+    return qce_set_error(QCE_ESTATE, "the last K-shard estimate had rows whose shifted sum underflowed and "
+                                     "qce_kshard_prepare ran before qce_kshard_finish: they cannot be recombined");
+  if (f0 > 0.0 && pend.mode == QCE_MODE_ALL) {
+    // exact recombination of the last step (every rank agrees through the MAX of the flag word)
+    KS_HIP(hipStreamWaitEvent(st, ks->ev_done, 0));
+    KS_RC(step_all(ks, pend.y, pend.B, pend.chunks, pend.scatter != 0, pend.h, st, true));
+    KS_HIP(hipEventRecord(ks->ev_done, ks->cs));
+    KS_HIP(hipStreamWaitEvent(st, ks->ev_done, 0));
+    KS_HIP(hipStreamSynchronize(st));
+  }
+  return QCE_OK;
+}
+
+int qce_kshard_timing(qce_kshard* ks, int enable) {
+  if (!ks) return qce_set_error(QCE_EARG, "null K-shard");
+  ks->timing = enable != 0;
+  ks->tev_used = 0;
+  return QCE_OK;
+}
+
+int qce_kshard_kernel_ms(qce_kshard* ks, double* total_ms, int* launches) {
+  if (!ks || !total_ms) return qce_set_error(QCE_EARG, "null argument");
+  DevGuard g(ks->device);
+  double t = 0.0;
+  for (size_t i = 0; i < ks->tev_used; ++i) {
+    KS_HIP(hipEventSynchronize(ks->tev[i].second));
+    float ms = 0.0f;
+    KS_HIP(hipEventElapsedTime(&ms, ks->tev[i].first, ks->tev[i].second));
+    t += ms;
+  }
+  *total_ms = t;
+  if (launches) *launches = (int)ks->tev_used;
+  ks->tev_used = 0;
+  return QCE_OK;
+}
+
+}  // extern "C"

@@ -136,10 +136,18 @@ class ComponentShardEstimator:
     [rows whose shifted sum underflowed, Cholesky failure on any rank]; with ``sync=False`` it returns without
     waiting for the device, and ``finish()`` (the caller's natural sync point) reads the flag word once, raises the
     reference's ValueError for a failed factorisation (gmm_cplx_bussgang.py:43-46) and recombines the flagged rows
-    exactly.  ``sync=True`` (default) is estimate + finish."""
+    exactly.  ``sync=True`` (default) is estimate + finish.
 
-    def __init__(self, means_cplx, covs_cplx, weights, rank, world, device=0, group=None, precision="f64"):
+    With ``comm`` (a ``_lib.Comm``, see ``make_comm``) the whole step runs inside the library (qce_kshard_*: the
+    collectives are RCCL calls of libqce, or a host transport), including the selective modes; without it the step
+    is orchestrated here over torch.distributed (the gloo rehearsal path of the CPU tests)."""
+
+    native = None  # the library's K-shard step (a _lib.KShard) when built with a communicator
+    _native_rows = None
+
+    def __init__(self, means_cplx, covs_cplx, weights, rank, world, device=0, group=None, precision="f64", comm=None):
         K = np.asarray(covs_cplx).shape[0]
+        self.K = K
         self.rank, self.world = rank, world
         self.lo, self.hi = component_slices(K, world)[rank]
         sl = slice(self.lo, self.hi)
@@ -154,6 +162,10 @@ class ComponentShardEstimator:
         self._pending = None
         self._flag_acc = None
         self._chol_local = False
+        if comm is not None:
+            if (comm.rank, comm.world) != (rank, world):
+                raise ValueError("communicator rank / world differ from the estimator's")
+            self.native = _lib.KShard(self.dev, comm, K)
 
     def _on_gpu(self):
         return getattr(self.dev, "device_type", "cuda") == "cuda"
@@ -164,6 +176,11 @@ class ComponentShardEstimator:
         on the prepare's stream, and the all-reduce is ordered behind it -- no host round trip per SNR point."""
         import torch
         import torch.distributed as dist
+        if self.native is not None:  # ordered on torch's current stream unless told otherwise (as estimate())
+            s = stream if stream is not None else torch.cuda.current_stream(torch.device("cuda", self.dev.device)
+                                                                            ).cuda_stream
+            self.native.prepare(A, snr_db, n_bits, quant_kind, thresholds, labels, stream=s)
+            return
         if self._on_gpu():
             dev = torch.device("cuda", self.dev.device)
             cur = torch.cuda.current_stream(dev)
@@ -214,16 +231,21 @@ class ComponentShardEstimator:
         return torch.tensor([1.0 if (local or math.isinf(float(self.shift))) else 0.0], dtype=torch.float64,
                             device=device)
 
-    def estimate(self, y, chunks=None, scatter=True, sync=True):
+    def estimate(self, y, chunks=None, scatter=True, sync=True, mode=_lib.MODE_ALL, param=0.0):
         """'all'-mode estimates of y (B, M) complex128 tensor.
 
         scatter=True: reduce-scatter per chunk, returns (rows, h) with h (n, N) complex128 the estimates of
         this rank's rows (global row indices `rows`, a LongTensor); scatter=False: all-reduce, every rank
         gets h for all B rows (rows = None).  The partial kernels run on torch's current stream, each
         chunk's collective asynchronously on RCCL's stream behind it.  sync=False: no host synchronisation; call
-        finish() before reading h (rows whose shifted sum underflowed are NaN until then)."""
+        finish() before reading h (rows whose shifted sum underflowed are NaN until then).  mode / param: the
+        reference's selective modes (gmm_cplx_bussgang.py:197-219, :229-242) on the native path (comm=...)."""
         import torch
         import torch.distributed as dist
+        if self.native is not None:
+            return self._estimate_native(y, chunks, scatter, sync, mode, param)
+        if mode != _lib.MODE_ALL:
+            raise NotImplementedError("selective modes K-shard through the library's communicator (comm=...)")
         B = y.shape[0]
         W = 2 * self.N + 2
         dev = y.device
@@ -258,7 +280,9 @@ class ComponentShardEstimator:
         flags = torch.cat([bad.sum().to(torch.float64).reshape(1), self._chol_flag(dev)])
         if multi:
             dist.all_reduce(flags, op=dist.ReduceOp.MAX, group=self.group)
-        self._flag_acc = flags if self._flag_acc is None else torch.maximum(self._flag_acc, flags)
+        if self._pending is not None:  # the step it supersedes can no longer be repaired: keep its flags apart
+            prev = self._pending[5]
+            self._flag_acc = prev if self._flag_acc is None else torch.maximum(self._flag_acc, prev)
         h = _packed_to_complex(rows)
         idx = torch.cat([torch.arange(a, max(a, b), device=dev) for a, b, _ in pieces]) if use_rs else None
         self._pending = (y, use_rs, bad, idx, h, flags)
@@ -270,19 +294,41 @@ class ComponentShardEstimator:
         """Read the flag words of the steps since the last finish() (one host sync): raise ValueError with the
         reference's message if a Cholesky factorisation failed on any rank, recombine the underflowed rows of the
         latest result exactly (in place) and return it as (rows, h)."""
+        if self.native is not None:
+            if self._native_rows is None:
+                return None
+            idx, h = self._native_rows
+            self._native_rows = None
+            self.native.finish()
+            return idx, h
         if self._pending is None:
             return None
         y, use_rs, bad, idx, h, flags = self._pending
-        acc = self._flag_acc
+        prev = self._flag_acc
         self._pending = self._flag_acc = None
-        f_last, f_any = flags.tolist(), acc.tolist()
-        if f_any[1] > 0:
+        f_last = flags.tolist()
+        f_prev = prev.tolist() if prev is not None else [0.0, 0.0]
+        if f_last[1] > 0 or f_prev[1] > 0:
             raise ValueError(_lib.CHOL_MESSAGE)
-        if f_any[0] > f_last[0]:
+        if f_prev[0] > 0:
             raise RuntimeError("an earlier K-shard estimate had rows whose shifted sum underflowed; estimate it "
                                "with sync=True to have them recombined")
         if f_last[0] > 0:
             self._repair(y, use_rs, bad, idx, h)
+        return idx, h
+
+    def _estimate_native(self, y, chunks, scatter, sync, mode, param):
+        import torch
+        ch = default_chunks(self.world) if chunks is None else chunks
+        stream = torch.cuda.current_stream(y.device).cuda_stream
+        ranges, h = self.native.estimate(y, mode, param, chunks=ch, scatter=scatter, stream=stream)
+        idx = None
+        if scatter:
+            idx = torch.cat([torch.arange(a, b, device=y.device) for a, b in ranges]) if ranges else \
+                torch.empty(0, dtype=torch.int64, device=y.device)
+        self._native_rows = (idx, h)
+        if sync:
+            return self.finish()
         return idx, h
 
     def _repair(self, y, use_rs, bad, idx, h):
@@ -316,6 +362,38 @@ class ComponentShardEstimator:
             h[mine] = hx[pos]
         else:
             h[grows] = hx
+
+
+def make_comm(rank, world, device=0, kind="rccl", group=None):
+    """The libqce communicator of this rank.  kind "rccl": rank 0's ncclUniqueId is shared over the initialised
+    torch.distributed group (any backend; gloo suffices), then every rank runs ncclCommInitRank on its device;
+    kind "host": collectives through torch.distributed on host tensors (gloo), staged by the library."""
+    import torch
+    import torch.distributed as dist
+    if kind == "rccl":
+        obj = [_lib.Comm.unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(obj, src=0, group=group)
+        return _lib.Comm(obj[0], rank, world, device)
+    if kind != "host":
+        raise ValueError(f"unknown communicator kind {kind!r}")
+
+    def fn(op, send, recv):
+        ts, tr = torch.from_numpy(send), torch.from_numpy(recv)
+        if op in (_lib.COLL_ALLREDUCE_SUM, _lib.COLL_ALLREDUCE_MAX):
+            tr.copy_(ts)
+            dist.all_reduce(tr, op=dist.ReduceOp.SUM if op == _lib.COLL_ALLREDUCE_SUM else dist.ReduceOp.MAX,
+                            group=group)
+        elif op == _lib.COLL_REDUCE_SCATTER_SUM:
+            tot = ts.clone()
+            dist.all_reduce(tot, op=dist.ReduceOp.SUM, group=group)  # gloo has no reduce_scatter
+            n = tr.numel()
+            tr.copy_(tot[rank * n:(rank + 1) * n])
+        elif op == _lib.COLL_ALLGATHER:
+            dist.all_gather(list(tr.chunk(world)), ts, group=group)
+        else:
+            raise ValueError(op)
+    return _lib.Comm.host(rank, world, device, fn)
 
 
 class BatchShardEstimator:

@@ -363,3 +363,73 @@ def test_bench_launcher_gloo_world2():
     d = json.loads(line[0])
     assert d["world_size"] == 2 and d["n_gpus"] == 2 and sorted(d["ranks"]) == [0, 1]
     assert abs(d["max_elapsed"] - 0.02) < 1e-12
+
+
+def _two_flagged_worker(rank, world, port, q):
+    """two sync=False steps that both have flagged rows -- the first one was superseded (its h already
+    handed back with NaN rows), so finish() must raise instead of silently repairing only the last step."""
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import sys
+    sys.path.insert(0, ROOT)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    fx = load_model("fullmean")
+    est = _make_est(rank, world, fx, "b1_5")
+    est.prepare(None, 0.0, 1)
+    est.shift += 900.0  # every row flagged, in both steps
+    y = torch.from_numpy(est.dev.y)
+    est.estimate(y, chunks=2, scatter=True, sync=False)
+    est.estimate(y, chunks=2, scatter=True, sync=False)
+    msg = None
+    try:
+        est.finish()
+    except RuntimeError as e:
+        msg = str(e)
+    # a single flagged step is still repaired exactly
+    est.estimate(y, chunks=2, scatter=True, sync=False)
+    rows, h = est.finish()
+    err = rel_fro(h.numpy(), est.dev.h[rows.numpy()])
+    dist.destroy_process_group()
+    q.put((rank, msg, err))
+
+
+def test_kshard_superseded_flagged_step_raises_gloo():
+    def check(res):
+        for rank, msg, err in res:
+            assert msg is not None and "earlier K-shard estimate" in msg, (rank, msg)
+            assert err < 1e-12, (rank, err)
+    _run(_two_flagged_worker, 2, (), check)
+
+
+def test_library_kshard_layout_matches_python():
+    """qce_kshard_rows / qce_kshard_slice (host-only entry points of the library's K-shard step) give the same
+    component split and per-rank row layout as sharding.component_slices / chunk_bounds."""
+    from quantized_channel_estimation_amd import _lib, build
+    from quantized_channel_estimation_amd.sharding import chunk_bounds, component_slices
+    build.build()
+    for K in (2, 7, 128, 256):
+        for world in (1, 2, 3, 8):
+            if K < world:
+                continue
+            for r in range(world):
+                assert _lib.kshard_slice(K, world, r) == component_slices(K, world)[r]
+    for B in (1, 7, 100, 1001, 100000):
+        for world in (1, 2, 3, 8):
+            for ch in (1, 2, 3, 4):
+                for sc in (True, False):
+                    b = chunk_bounds(B, ch, world, sc)
+                    seen = []
+                    for r in range(world):
+                        lib = _lib.kshard_rows(B, ch, world, r, sc)
+                        assert len(lib) == len(b)
+                        for (lo, hi), (a, e) in zip(b, lib):
+                            if sc:
+                                q = -(-(hi - lo) // world)
+                                assert a == lo + r * q and e == min(hi, a + q) or (e == a and a >= hi)
+                            else:
+                                assert (a, e) == (lo, hi)
+                        seen += [i for a, e in lib for i in range(a, e)]
+                    if sc:
+                        assert sorted(seen) == list(range(B))

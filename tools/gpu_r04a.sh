@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round 4: the library's K-shard step (qce_kshard_*) on the GPU -- world-1 RCCL and 2/3-rank host-transport tests,
+# then a kernel trace of the world-1 RCCL metric step (RCCL kernels beside the estimate kernels).
+set -o pipefail
+mkdir -p gpurun_out/r04a
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 600 python -u -m pytest tests/test_gpu_kshard_native.py -x -v --timeout 170 --timeout-method thread > gpurun_out/r04a/pytest.log 2>&1 || { tail -40 gpurun_out/r04a/pytest.log; exit 1; }
+tail -3 gpurun_out/r04a/pytest.log
+timeout -k 10 300 python -u tools/kshard_native_step.py > gpurun_out/r04a/step.json 2> gpurun_out/r04a/step.err || { tail -30 gpurun_out/r04a/step.err; exit 1; }
+cat gpurun_out/r04a/step.json
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/r04a/prof -o trace -- python3 tools/kshard_native_step.py --steps 5 > gpurun_out/r04a/prof.log 2> gpurun_out/r04a/prof.err || { tail -30 gpurun_out/r04a/prof.err; exit 1; }
+find gpurun_out/r04a/prof -name "*kernel_stats.csv" | head -3

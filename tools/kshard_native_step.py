@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""One rank's K-shard step through the library's communicator (qce_kshard_*) at the metric geometry, world 1 over
+RCCL by default: prepare (+ shift MAX all-reduce), chunked partials + reduce-scatters, flag MAX, finish.  Prints one
+JSON line (per-step time, summed partial-kernel time, parity of 512 rows against the FP64 oracle).  Used under
+rocprofv3 --kernel-trace to show the RCCL kernels next to the estimate kernels (profiles/r04_kshard_native_*)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--K", type=int, default=128)
+    ap.add_argument("--N", type=int, default=64)
+    ap.add_argument("--B", type=int, default=100_000)
+    ap.add_argument("--chunks", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--kind", default="rccl", choices=["rccl", "host"])
+    a = ap.parse_args()
+    import torch
+    from quantized_channel_estimation_amd import inputs
+    from quantized_channel_estimation_amd.sharding import ComponentShardEstimator, make_comm
+    means, covs, w = inputs.synthetic_model(a.K, a.N)
+    rng = np.random.default_rng(5)
+    hp, _ = inputs.scm_generate(2048, 1, a.N, rng, n_path=3)
+    h = hp[:, 0, :].astype(complex)[rng.integers(0, 2048, size=a.B)]
+    y = np.ascontiguousarray(inputs.get_observation_nbit(h, 5.0, None, 1, rng=rng), dtype=np.complex128)
+    torch.cuda.set_device(0)
+    if a.kind == "host":
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    comm = make_comm(0, 1, 0, kind=a.kind)
+    est = ComponentShardEstimator(means, covs, w, 0, 1, device=0, comm=comm)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    yd = torch.from_numpy(y).cuda()
+    for _ in range(2):
+        est.prepare(None, 5.0, 1)
+        est.estimate(yd, chunks=a.chunks, scatter=True, sync=False)
+    est.finish()
+    torch.cuda.synchronize()
+    est.native.timing(True)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        est.prepare(None, 5.0, 1)
+        res = est.estimate(yd, chunks=a.chunks, scatter=True, sync=False)
+    rows, hk = est.finish()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    kms, nl = est.native.kernel_ms()
+    from oracle import qce_oracle as O
+    r = rows.cpu().numpy()[:512]
+    ho = O.estimate(means, covs, w, y[r], 5.0, a.N, None, "all", 1)
+    err = float(np.linalg.norm(hk[:512].cpu().numpy() - ho) / np.linalg.norm(ho))
+    print(json.dumps(dict(kind=a.kind, K=a.K, N=a.N, B=a.B, chunks=a.chunks, steps=a.steps, ms_per_step=dt * 1e3,
+                          partial_kernel_ms_per_step=kms / a.steps, launches=nl, est_per_s=a.B / dt,
+                          parity_rel_fro=err)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
