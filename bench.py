@@ -74,6 +74,8 @@ def parse():
                          "backend (nccl = RCCL through torch, gloo) driving sharding.py's Python orchestration")
     ap.add_argument("--collective", default="rs", choices=["rs", "ar"],
                     help="K-shard SUM collective: reduce-scatter (rank keeps its rows) or all-reduce")
+    ap.add_argument("--single-buffer", action="store_true",
+                    help="native K-shard: one table set (no overlap of the next prepare with the current step)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU-baseline budget per leg (0 = skip)")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the fast-path side line")
@@ -487,7 +489,7 @@ def main():
         from quantized_channel_estimation_amd.sharding import make_comm
         comm = make_comm(rank, world, local, kind="rccl")
         shard = ComponentShardEstimator(means, covs, w, rank, world, device=local, precision=args.precision,
-                                        comm=comm)
+                                        comm=comm, double_buffer=not args.single_buffer)
         dm = shard.dev
 
         def step(ev=None):
@@ -584,14 +586,23 @@ def main():
     kern_tag = "fft" if dm.structure()[2] else ("f64" if dtype_of(dm) == "f64" else "h2")
     traffic = None
     tpath = args.traffic or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    traffic_note = None
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
-            if tj.get("config") == args.config and tj.get("B") == B and tj.get("kernel") == kern_tag:
+            if tj.get("build_id") != _lib.build_id():
+                # a PMC measurement of another build of the kernel is not this kernel's traffic
+                traffic_note = f"{os.path.basename(tpath)} is from build {tj.get('build_id')}, not {_lib.build_id()}"
+            elif tj.get("config") == args.config and tj.get("B") == B and tj.get("kernel") == kern_tag \
+                    and not kshard:
                 traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+        except Exception as e:
+            traffic, traffic_note = None, f"unreadable traffic file: {e}"
     roofline = roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic)
+    if traffic is not None:
+        roofline["traffic_source"] = os.path.relpath(tpath, ROOT) + " (rocprofv3 PMC of this build)"
+    elif traffic_note:
+        roofline["traffic_note"] = traffic_note
 
     extras = {}
     if rank == 0 and world == 1 and not args.no_extras and args.config == "metric":

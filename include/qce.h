@@ -70,8 +70,9 @@ int qce_device_count(int* count);
 
 /* Model parameters after `Gmm_nbit.fit` (gmm_cplx_bussgang.py:96-163): means_cplx (K,N) c128,
  * covs_cplx (K,N,N) c128, gm.weights_ (K,) f64.  Replaces the attribute bag the reference keeps in
- * its sklearn GaussianMixture (:86-94).  N <= 256 (padded internally to 16/32/64/128/256), K <= 256 for
- * the selective modes.  The structure of the covariances is detected here (qce_model_structure). */
+ * its sklearn GaussianMixture (:86-94).  N <= 256 (padded internally to 16/32/64/128/256), K <= 4096 for
+ * the selective modes and the proba / labels outputs (any K for 'all').  The structure of the covariances is
+ * detected here (qce_model_structure). */
 int qce_model_create(int K, int N, const double* means_cplx, const double* covs_cplx, const double* weights,
                      int device, qce_model** out);
 int qce_model_destroy(qce_model* model);
@@ -279,6 +280,11 @@ int qce_kshard_rows(int64_t B, int chunks, int world, int rank, int scatter, int
  * created from that slice), `comm` its communicator.  Neither is owned. */
 int qce_kshard_create(qce_model* shard, qce_comm* comm, int K_total, qce_kshard** out);
 int qce_kshard_destroy(qce_kshard* ks);
+/* Double-buffered tables: `spare` is a second model of the same shard (same parameters; not owned).  Prepares then
+ * alternate between the two table sets on the library's prepare stream: prepare t+1 waits only for the last step
+ * that read its set (step t-1), so it runs beside step t's partial kernels (Bussgang_GMM.py:284-287: the next SNR
+ * point's tables do not depend on the current estimate); its shift MAX is ordered after step t's collectives. */
+int qce_kshard_set_spare(qce_kshard* ks, qce_model* spare);
 /* Per-SNR prepare of the shard (qce_prepare) and the shared shift M* = max over ALL components of
  * c_k = -M log(pi) + 2 log det P_k + log w_k (>= every lp: the quad form is >= 0), one MAX all-reduce on `stream`
  * that also carries every rank's Cholesky status (+inf).  No host synchronisation (host transports aside). */

@@ -90,6 +90,7 @@ SIGNATURES = {
                                        ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     "qce_kshard_create": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.POINTER(_vp)]),
     "qce_kshard_destroy": (ctypes.c_int, [_vp]),
+    "qce_kshard_set_spare": (ctypes.c_int, [_vp, _vp]),
     "qce_kshard_prepare": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_double, ctypes.c_double, ctypes.c_int, _vp,
                                           _vp, ctypes.c_int, _vp]),
     "qce_kshard_estimate": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_int,
@@ -497,6 +498,11 @@ class KShard:
         check(load().qce_kshard_create(model.handle, comm.handle, int(K_total), ctypes.byref(h)))
         self._h, self.model, self.comm, self.K = h, model, comm, int(K_total)
         self._keep = None
+
+    def set_spare(self, spare):
+        """Double-buffered tables: `spare` another DeviceModel of the same shard (qce_kshard_set_spare)."""
+        check(load().qce_kshard_set_spare(self._h, spare.handle))
+        self.spare = spare
 
     def close(self):
         if getattr(self, "_h", None):

@@ -1031,7 +1031,8 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
   if (B == 0) return QCE_OK;
   if (!m->fft_active && mode != QCE_MODE_ALL && !qce_select_shape_supported(m->MP, m->NP))
     return fail(QCE_ENOTIMPL, "selective modes: shape not covered");
-  if (mode != QCE_MODE_ALL && m->K > 256) return fail(QCE_ENOTIMPL, "selective modes support K <= 256");
+  if (mode != QCE_MODE_ALL && m->K > qce_select_max_k())
+    return fail(QCE_ENOTIMPL, "selective modes support K <= " + std::to_string(qce_select_max_k()));
   DeviceGuard g(m->device);
   hipStream_t st = pick_stream(m, stream);
   if (io == QCE_IO_HOST)
@@ -1125,7 +1126,8 @@ int qce_log_prob(qce_model* m, const double* X, int64_t B, double* lp_out, doubl
   if (rc) return rc;
   if (B < 0 || (B > 0 && !X)) return fail(QCE_EARG, "bad X");
   if (B == 0) return QCE_OK;
-  if (m->K > 256 && (proba_out || labels_out)) return fail(QCE_ENOTIMPL, "proba/labels support K <= 256");
+  if (m->K > qce_select_max_k() && (proba_out || labels_out))
+    return fail(QCE_ENOTIMPL, "proba/labels support K <= " + std::to_string(qce_select_max_k()));
   DeviceGuard g(m->device);
   hipStream_t st = pick_stream(m, stream);
   const double2* dx = nullptr;

@@ -379,6 +379,132 @@ __global__ __launch_bounds__(256) void k_select(long long B, int K, const double
 }
 
 // ---------------------------------------------------------------------------
+// k_select for K > 256 (up to QCE_SELECT_WIDE_MAX): one 256-thread workgroup per sample, the row in LDS.
+// Same results as k_select: labels = first maximum of lp (numpy argmax), proba = exp(lp - logsumexp);
+// top-n / cumulative-p select in descending-proba order with ties towards the higher index (a bitonic sort of
+// (proba, index) keys in LDS), the cumulative sum taken sequentially in that order (np.cumsum + searchsorted,
+// gmm_cplx_bussgang.py:213, :235-236), weights renormalised by the selected sum (:219, :242).
+// ---------------------------------------------------------------------------
+#define QCE_SELECT_WIDE_MAX 4096
+
+QCE_DEV bool sel_before(double va, int ia, double vb, int ib) { return va > vb || (va == vb && ia > ib); }
+
+__global__ __launch_bounds__(256) void k_select_wide(long long B, int K, int P, const double* __restrict__ lp,
+                                                     int mode, int nsel, double psel, double* __restrict__ proba,
+                                                     long long* __restrict__ labels, float* __restrict__ wts,
+                                                     double* __restrict__ wts64) {
+  extern __shared__ double sel_lds[];
+  double* v = sel_lds;                                // P values
+  int* id = reinterpret_cast<int*>(sel_lds + P);      // P indices
+  __shared__ double rv[4];
+  __shared__ int ri[4];
+  __shared__ double s_tot;
+  __shared__ int s_cnt;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const long long b = blockIdx.x;
+  const double* row = lp + b * K;
+  // max and first argmax
+  double bv = QCE_NEG_INF;
+  int bi = 1 << 30;
+  for (int k = tid; k < K; k += 256) {
+    const double x = row[k];
+    v[k] = x;
+    if (x > bv || bi == (1 << 30)) {
+      bv = x;
+      bi = k;
+    }
+  }
+  wave_argmax(bv, bi, true);
+  if (lane == 0) {
+    rv[wv] = bv;
+    ri[wv] = bi;
+  }
+  __syncthreads();
+  bv = rv[0];
+  bi = ri[0];
+  for (int w = 1; w < 4; ++w)
+    if (rv[w] > bv || (rv[w] == bv && ri[w] < bi)) {
+      bv = rv[w];
+      bi = ri[w];
+    }
+  if (labels && tid == 0) labels[b] = bi;
+  const double mx = bv;
+  double t = 0.0;
+  for (int k = tid; k < K; k += 256) t += exp(v[k] - mx);
+  t = wave_sum(t);
+  __syncthreads();
+  if (lane == 0) rv[wv] = t;
+  __syncthreads();
+  const double lse = log(rv[0] + rv[1] + rv[2] + rv[3]) + mx;
+  for (int k = tid; k < K; k += 256) {
+    const double pr = exp(v[k] - lse);
+    if (proba) proba[b * K + k] = pr;
+    v[k] = pr;
+    id[k] = k;
+  }
+  if (!wts && !wts64) return;
+  if (mode == 3 || (mode == 1 && nsel == 1)) {  // argmax path: weight exactly 1 on the first maximum
+    for (int k = tid; k < K; k += 256) {
+      const double w = (k == bi) ? 1.0 : 0.0;
+      if (wts) wts[b * K + k] = (float)w;
+      if (wts64) wts64[b * K + k] = w;
+    }
+    return;
+  }
+  for (int k = K + tid; k < P; k += 256) {
+    v[k] = -2.0;  // below every probability
+    id[k] = -1;
+  }
+  __syncthreads();
+  // bitonic sort, descending by (proba, index)
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < P; i += 256) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const bool desc = (i & size) == 0;
+          const double va = v[i], vb = v[j];
+          const int ia = id[i], ib = id[j];
+          if (desc ? sel_before(vb, ib, va, ia) : sel_before(va, ia, vb, ib)) {
+            v[i] = vb;
+            v[j] = va;
+            id[i] = ib;
+            id[j] = ia;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (tid == 0) {  // sequential prefix in the sorted order
+    int cnt = (mode == 1) ? (nsel < K ? nsel : K) : K;
+    double cum = 0.0;
+    if (mode == 2) {
+      for (int j = 0; j < K; ++j) {
+        cum += v[j];
+        if (cum >= psel) {
+          cnt = j + 1;
+          break;
+        }
+      }
+    }
+    double tot = 0.0;
+    for (int j = 0; j < cnt; ++j) tot += v[j];
+    s_cnt = cnt;
+    s_tot = tot;
+  }
+  __syncthreads();
+  const int cnt = s_cnt;
+  const double tot = s_tot;
+  for (int j = tid; j < K; j += 256) {  // every component sits at exactly one sorted position
+    const double w = j < cnt ? v[j] / tot : 0.0;
+    const int k = id[j];
+    if (wts) wts[b * K + k] = (float)w;
+    if (wts64) wts64[b * K + k] = w;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // dispatch
 // ---------------------------------------------------------------------------
 bool qce_shape_supported(int MP, int NP) {  // the FP32 fused 'all' kernel (k_est_all_f32)
@@ -471,9 +597,19 @@ hipError_t qce_launch_lp(const QceEstArgs& a, double* lp, hipStream_t st) {
   }
 }
 
+int qce_select_max_k() { return QCE_SELECT_WIDE_MAX; }
+
 hipError_t qce_launch_select(long long B, int K, const double* lp, int mode, int n, double p, double* proba,
                              long long* labels, float* wts, hipStream_t st, double* wts64) {
-  if (K > 256) return hipErrorInvalidValue;
+  if (K > 256) {
+    if (K > QCE_SELECT_WIDE_MAX) return hipErrorInvalidValue;
+    int P = 1;
+    while (P < K) P <<= 1;
+    const size_t lds = (size_t)P * (sizeof(double) + sizeof(int));
+    hipLaunchKernelGGL(k_select_wide, dim3((unsigned)B), dim3(256), lds, st, B, K, P, lp, mode, n, p, proba, labels, wts,
+                       wts64);
+    return hipGetLastError();
+  }
   dim3 grid((unsigned)((B + 3) / 4));
   hipLaunchKernelGGL(k_select, grid, dim3(256), 0, st, B, K, lp, mode, n, p, proba, labels, wts, wts64);
   return hipGetLastError();

@@ -49,6 +49,7 @@ hipError_t qce_launch_lp(const QceEstArgs& a, double* lp, hipStream_t st);
 // selection: mode 0 = proba only, 1 = top-n, 2 = cumulative-p, 3 = argmax(lp)
 hipError_t qce_launch_select(long long B, int K, const double* lp, int mode, int n, double p, double* proba,
                              long long* labels, float* wts, hipStream_t st, double* wts64 = nullptr);
+int qce_select_max_k();  // widest K qce_launch_select covers (k_select up to 256, k_select_wide beyond)
 // FP64 selective-mode LMMSE h = sum_k w64[b][k] (W_k y + b_k), w64 sparse; WT (K x M x N) = transposed filters
 // (built from W when transpose, else reused)
 hipError_t qce_launch_sparse_f64(long long B, int N, int M, int K, const double2* y, const double* w, const double2* W,

@@ -286,14 +286,21 @@ struct qce_comm {
 };
 
 struct qce_kshard {
-  qce_model* m = nullptr;  // not owned; never dereferenced by qce_kshard_destroy (the model may already be gone)
-  int device = 0;
+  qce_model* m = nullptr;  // the model of the latest prepare (mods[cur]); not owned, never dereferenced by
+  int device = 0;          // qce_kshard_destroy (the model may already be gone)
+  // double-buffered tables (qce_kshard_set_spare): prepare t+1 fills the other model on the prepare stream `ps`
+  // while step t's partial kernels still read this one
+  qce_model* mods[2] = {nullptr, nullptr};
+  int cur = 0;
+  hipStream_t ps = nullptr;
+  hipEvent_t ev_prep[2] = {nullptr, nullptr}, ev_used[2] = {nullptr, nullptr};
+  int used_valid[2] = {0, 0};
   qce_comm* c = nullptr;
   int K = 0, lo = 0, hi = 0, Kmax = 0;
   hipStream_t cs = nullptr;  // communication stream: the chunks' collectives and row finalisation
   std::vector<hipEvent_t> ev_chunk;
   hipEvent_t ev_done = nullptr;
-  KBuf<double> shift, fl, earlier, pk, rs;
+  KBuf<double> shift, fl, earlier, pk, rs;  // shift: one slot per table set
   KBuf<unsigned> cnt;
   double* host_fl = nullptr;  // pinned: [fl0, fl1, earlier0, earlier1] of the last step
   int local_chol = 0;         // this rank's library refused a call with the reference's Cholesky error
@@ -304,6 +311,7 @@ struct qce_kshard {
     long long B = 0;
     int chunks = 1, scatter = 1, mode = QCE_MODE_ALL;
     double2* h = nullptr;
+    qce_model* model = nullptr;  // the table set the step read
     int stale = 0;  // a prepare ran after the step: its rows can no longer be recombined with the step's tables
   } pending;
   int any_pending_before = 0;  // a step was superseded before finish(): its flags went into `earlier`
@@ -404,7 +412,7 @@ int timed_end(qce_kshard* ks, hipStream_t st) {
 int reduce_chunks(qce_kshard* ks, const std::vector<Chunk>& L, bool scatter, int W, hipStream_t st, double2* h_out,
                   bool count_flags, size_t chunk_index) {
   qce_comm* c = ks->c;
-  const int N = ks->m->N;
+  const int N = ks->m->N;  // every table set has the same N
   const Chunk& ch = L[chunk_index];
   hipEvent_t ev = ks->ev_chunk[chunk_index];
   KS_HIP(hipEventRecord(ev, st));
@@ -439,7 +447,8 @@ int ensure_events(qce_kshard* ks, size_t n) {
 
 // close a step: flag word MAX, pinned copy of [fl, earlier], the caller's stream ordered behind the comm stream
 int close_step(qce_kshard* ks, hipStream_t st) {
-  hipLaunchKernelGGL(k_ks_flags, dim3(1), dim3(64), 0, ks->cs, ks->cnt.p, ks->shift.p, ks->local_chol, ks->fl.p);
+  hipLaunchKernelGGL(k_ks_flags, dim3(1), dim3(64), 0, ks->cs, ks->cnt.p, ks->shift.p + ks->cur, ks->local_chol,
+                     ks->fl.p);
   KS_HIP(hipGetLastError());
   KS_RC(collective(ks->c, QCE_COLL_ALLREDUCE_MAX, ks->fl.p, ks->fl.p, 2, ks->cs));
   KS_HIP(hipMemcpyAsync(ks->host_fl, ks->fl.p, 2 * sizeof(double), hipMemcpyDeviceToHost, ks->cs));
@@ -451,9 +460,8 @@ int close_step(qce_kshard* ks, hipStream_t st) {
 
 // 'all' mode: per chunk the shifted partial on st (or, for the exact recombination, the per-row-shift rows of a
 // whole-batch FP64 partial), its SUM collective on cs, the finalisation
-int step_all(qce_kshard* ks, const double2* y, long long B, int chunks, bool scatter, double2* h, hipStream_t st,
-             bool rowshift) {
-  qce_model* m = ks->m;
+int step_all(qce_kshard* ks, qce_model* m, const double2* y, long long B, int chunks, bool scatter, double2* h,
+             hipStream_t st, bool rowshift) {
   qce_comm* c = ks->c;
   const int N = m->N, M = m->M, W = 2 * N + 2;
   std::vector<Chunk> L = chunk_layout(B, chunks, c->world, c->rank, scatter);
@@ -494,7 +502,7 @@ int step_all(qce_kshard* ks, const double2* y, long long B, int chunks, bool sca
       if (!ks->local_chol) {
         KS_RC(timed_begin(ks, st));
         ok = guarded(ks, qce_estimate_partial_shifted(m, reinterpret_cast<const double*>(y + ch.lo * M), n,
-                                                      ks->shift.p, pk, QCE_IO_DEVICE, st), &hard);
+                                                      ks->shift.p + ks->cur, pk, QCE_IO_DEVICE, st), &hard);
         if (hard) return hard;
         KS_RC(timed_end(ks, st));
       }
@@ -523,7 +531,8 @@ int step_select(qce_kshard* ks, const double2* y, long long B, int mode, double 
   } else {
     return qce_set_error(QCE_EARG, "unknown mode");
   }
-  if (kmode != 3 && ks->K > 256) return qce_set_error(QCE_ENOTIMPL, "K-shard top-n / cumulative-p support K <= 256");
+  if (kmode != 3 && ks->K > qce_select_max_k())
+    return qce_set_error(QCE_ENOTIMPL, "K-shard top-n / cumulative-p support K <= " + std::to_string(qce_select_max_k()));
   std::vector<Chunk> L = chunk_layout(B, 1, c->world, c->rank, scatter);
   KS_RC(ensure_events(ks, 1));
   const long long npad = L[0].npad;
@@ -699,6 +708,7 @@ int qce_kshard_create(qce_model* shard, qce_comm* comm, int K_total, qce_kshard*
   DevGuard g(shard->device);
   qce_kshard* ks = new qce_kshard();
   ks->m = shard;
+  ks->mods[0] = shard;
   ks->device = shard->device;
   ks->c = comm;
   ks->K = K_total;
@@ -707,7 +717,7 @@ int qce_kshard_create(qce_model* shard, qce_comm* comm, int K_total, qce_kshard*
   ks->Kmax = (K_total + comm->world - 1) / comm->world;
   hipError_t e = hipStreamCreateWithFlags(&ks->cs, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ks->ev_done, hipEventDisableTiming);
-  if (e == hipSuccess) e = ks->shift.ensure(1);
+  if (e == hipSuccess) e = ks->shift.ensure(2);
   if (e == hipSuccess) e = ks->fl.ensure(2);
   if (e == hipSuccess) e = ks->earlier.ensure(2);
   if (e == hipSuccess) e = ks->cnt.ensure(1);
@@ -736,6 +746,14 @@ int qce_kshard_destroy(qce_kshard* ks) {
     (void)hipEventDestroy(pr.second);
   }
   if (ks->ev_done) (void)hipEventDestroy(ks->ev_done);
+  for (int i = 0; i < 2; ++i) {
+    if (ks->ev_prep[i]) (void)hipEventDestroy(ks->ev_prep[i]);
+    if (ks->ev_used[i]) (void)hipEventDestroy(ks->ev_used[i]);
+  }
+  if (ks->ps) {
+    (void)hipStreamSynchronize(ks->ps);
+    (void)hipStreamDestroy(ks->ps);
+  }
   if (ks->host_fl) (void)hipHostFree(ks->host_fl);
   if (ks->cs) (void)hipStreamDestroy(ks->cs);
   delete ks;
@@ -747,21 +765,51 @@ int qce_kshard_prepare(qce_kshard* ks, const double* A, int M, double snr_db, do
   if (!ks) return qce_set_error(QCE_EARG, "null K-shard");
   DevGuard g(ks->device);
   hipStream_t st = ks_stream(ks, stream);
+  const bool dbl = ks->mods[1] != nullptr;
+  // with a spare table set the prepare fills the set the previous step did NOT read, on the prepare stream, so it
+  // overlaps that step's partial kernels; it waits only for the last step that read this set
+  const int j = dbl ? 1 - ks->cur : 0;
+  qce_model* m = ks->mods[j];
+  hipStream_t ps = dbl ? ks->ps : st;
+  if (dbl) {
+    KS_HIP(hipStreamWaitEvent(ps, ks->ev_done, 0));  // no-op before the first step; orders any repair of that step
+    if (ks->used_valid[j]) KS_HIP(hipStreamWaitEvent(ps, ks->ev_used[j], 0));
+  }
+  if (ks->pending.valid && ks->pending.model == m) ks->pending.stale = 1;  // its tables are being replaced
+  ks->cur = j;
+  ks->m = m;
   ks->local_chol = 0;
-  if (ks->pending.valid) ks->pending.stale = 1;  // an exact recombination would need the replaced tables
-  KS_RC(qce_prepare(ks->m, A, M, snr_db, n_bits, quant_kind, thresholds, labels, n_levels, st));
+  KS_RC(qce_prepare(m, A, M, snr_db, n_bits, quant_kind, thresholds, labels, n_levels, ps));
+  double* shift = ks->shift.p + j;
   int hard = QCE_OK;
-  if (!guarded(ks, qce_cconst_max(ks->m, ks->shift.p, QCE_IO_DEVICE, st), &hard)) {
+  if (!guarded(ks, qce_cconst_max(m, shift, QCE_IO_DEVICE, ps), &hard)) {
     if (hard) return hard;
     const double inf = __builtin_inf();  // the failure rides the shift as the kernel would have written it
-    KS_HIP(hipMemcpyAsync(ks->shift.p, &inf, sizeof(double), hipMemcpyHostToDevice, st));
-    KS_HIP(hipStreamSynchronize(st));
+    KS_HIP(hipMemcpyAsync(shift, &inf, sizeof(double), hipMemcpyHostToDevice, ps));
+    KS_HIP(hipStreamSynchronize(ps));
   }
-  KS_RC(collective(ks->c, QCE_COLL_ALLREDUCE_MAX, ks->shift.p, ks->shift.p, 1, st));
+  // the shift MAX is ordered after the previous step's collectives (ev_done above): one communicator, one order
+  KS_RC(collective(ks->c, QCE_COLL_ALLREDUCE_MAX, shift, shift, 1, ps));
   if (const char* b = getenv("QCE_KSHARD_SHIFT_BIAS")) {  // tests only: force the underflow path
-    hipLaunchKernelGGL(k_ks_add, dim3(1), dim3(64), 0, st, ks->shift.p, atof(b));
+    hipLaunchKernelGGL(k_ks_add, dim3(1), dim3(64), 0, ps, shift, atof(b));
     KS_HIP(hipGetLastError());
   }
+  if (dbl) KS_HIP(hipEventRecord(ks->ev_prep[j], ps));
+  return QCE_OK;
+}
+
+int qce_kshard_set_spare(qce_kshard* ks, qce_model* spare) {
+  if (!ks || !spare) return qce_set_error(QCE_EARG, "null argument");
+  const qce_model* a = ks->mods[0];
+  if (spare == a || spare->K != a->K || spare->N != a->N || spare->device != a->device)
+    return qce_set_error(QCE_EARG, "the spare model must be a second model of the same shard (same K, N, device)");
+  DevGuard g(ks->device);
+  KS_HIP(hipStreamCreateWithFlags(&ks->ps, hipStreamNonBlocking));
+  for (int i = 0; i < 2; ++i) {
+    KS_HIP(hipEventCreateWithFlags(&ks->ev_prep[i], hipEventDisableTiming));
+    KS_HIP(hipEventCreateWithFlags(&ks->ev_used[i], hipEventDisableTiming));
+  }
+  ks->mods[1] = spare;
   return QCE_OK;
 }
 
@@ -781,12 +829,18 @@ int qce_kshard_estimate(qce_kshard* ks, const double* y, int64_t B, int mode, do
   KS_HIP(hipMemsetAsync(ks->cnt.p, 0, sizeof(unsigned), ks->cs));
   const double2* yd = reinterpret_cast<const double2*>(y);
   double2* hd = reinterpret_cast<double2*>(h_out);
+  const bool dbl = ks->mods[1] != nullptr;
+  if (dbl) KS_HIP(hipStreamWaitEvent(st, ks->ev_prep[ks->cur], 0));
   if (B > 0) {
     if (mode == QCE_MODE_ALL) {
-      KS_RC(step_all(ks, yd, B, chunks, scatter != 0, hd, st, false));
+      KS_RC(step_all(ks, ks->m, yd, B, chunks, scatter != 0, hd, st, false));
     } else {
       KS_RC(step_select(ks, yd, B, mode, mode_param, scatter != 0, hd, st));
     }
+  }
+  if (dbl) {  // the table set's last reader: the next prepare into it waits for this
+    KS_HIP(hipEventRecord(ks->ev_used[ks->cur], st));
+    ks->used_valid[ks->cur] = 1;
   }
   KS_RC(close_step(ks, st));
   ks->pending.valid = 1;
@@ -796,6 +850,7 @@ int qce_kshard_estimate(qce_kshard* ks, const double* y, int64_t B, int mode, do
   ks->pending.scatter = scatter;
   ks->pending.mode = mode;
   ks->pending.h = hd;
+  ks->pending.model = ks->m;
   ks->pending.stale = 0;
   return QCE_OK;
 }
@@ -819,9 +874,11 @@ int qce_kshard_finish(qce_kshard* ks, void* stream) {
     return qce_set_error(QCE_ESTATE, "the last K-shard estimate had rows whose shifted sum underflowed and "
                                      "qce_kshard_prepare ran before qce_kshard_finish: they cannot be recombined");
   if (f0 > 0.0 && pend.mode == QCE_MODE_ALL) {
-    // exact recombination of the last step (every rank agrees through the MAX of the flag word)
+    // exact recombination of the last step (every rank agrees through the MAX of the flag word); ordered after
+    // any prepare already issued on the prepare stream (its MAX collective): one communicator, one order
     KS_HIP(hipStreamWaitEvent(st, ks->ev_done, 0));
-    KS_RC(step_all(ks, pend.y, pend.B, pend.chunks, pend.scatter != 0, pend.h, st, true));
+    if (ks->mods[1]) KS_HIP(hipStreamWaitEvent(st, ks->ev_prep[ks->cur], 0));
+    KS_RC(step_all(ks, pend.model, pend.y, pend.B, pend.chunks, pend.scatter != 0, pend.h, st, true));
     KS_HIP(hipEventRecord(ks->ev_done, ks->cs));
     KS_HIP(hipStreamWaitEvent(st, ks->ev_done, 0));
     KS_HIP(hipStreamSynchronize(st));

@@ -145,7 +145,8 @@ class ComponentShardEstimator:
     native = None  # the library's K-shard step (a _lib.KShard) when built with a communicator
     _native_rows = None
 
-    def __init__(self, means_cplx, covs_cplx, weights, rank, world, device=0, group=None, precision="f64", comm=None):
+    def __init__(self, means_cplx, covs_cplx, weights, rank, world, device=0, group=None, precision="f64", comm=None,
+                 double_buffer=False):
         K = np.asarray(covs_cplx).shape[0]
         self.K = K
         self.rank, self.world = rank, world
@@ -166,6 +167,11 @@ class ComponentShardEstimator:
             if (comm.rank, comm.world) != (rank, world):
                 raise ValueError("communicator rank / world differ from the estimator's")
             self.native = _lib.KShard(self.dev, comm, K)
+            if double_buffer:  # a second table set: the next prepare overlaps the current step (qce_kshard_set_spare)
+                spare = _lib.DeviceModel(means, np.asarray(covs_cplx)[sl], np.asarray(weights)[sl], device=device)
+                if precision != "f64":
+                    spare.set_precision(precision)
+                self.native.set_spare(spare)
 
     def _on_gpu(self):
         return getattr(self.dev, "device_type", "cuda") == "cuda"

@@ -151,20 +151,26 @@ def test_bench_kshard_two_ranks_gloo_one_gpu():
 
 
 @pytest.mark.gpu
-def test_size_limits():
-    """Shape limits of the C ABI: N > 256 is refused at model creation, the selective modes take K <= 256
-    (QCE_ENOTIMPL -> NotImplementedError), while 'all' mode runs any K (here 300, vs the FP64 oracle)."""
+@pytest.mark.parametrize("K", [300, 1000])
+def test_wide_k_all_modes(K):
+    """K beyond one wave's 256 components: 'all', argmax, top-3, cumulative-p 0.9, predict_proba and the labels
+    (k_select_wide: the row in LDS, a bitonic sort of (proba, index)) against the FP64 oracle
+    (gmm_cplx_bussgang.py:197-243, :335-367); N > 256 stays refused at model creation."""
     from oracle import qce_oracle as O
     from quantized_channel_estimation_amd import _lib, inputs
-    means, covs, w = inputs.synthetic_model(300, 16, seed=9)
+    means, covs, w = inputs.synthetic_model(K, 16, seed=9)
     rng = np.random.default_rng(9)
     y = (np.sign(rng.standard_normal((40, 16))) + 1j * np.sign(rng.standard_normal((40, 16)))) / np.sqrt(2)
     dm = _lib.DeviceModel(means, covs, w)
     dm.prepare(None, 5.0, 1.0)
-    h = dm.estimate(y)
-    assert rel_fro(h, O.estimate(means, covs, w, y, 5.0, 16, None, "all", 1)) < 1e-9
-    with pytest.raises(NotImplementedError):
-        dm.estimate(y, _lib.MODE_TOPN, 1.0)
+    for mode, (cm, param) in (("all", (_lib.MODE_ALL, 0.0)), (1, (_lib.MODE_TOPN, 1.0)), (3, (_lib.MODE_TOPN, 3.0)),
+                              (0.9, (_lib.MODE_CUMP, 0.9))):
+        h = dm.estimate(y, cm, param)
+        assert rel_fro(h, O.estimate(means, covs, w, y, 5.0, 16, None, mode, 1)) < 1e-9, mode
+    t = O.prepare(means, covs, np.eye(16), 5.0, 1)
+    lp, pr, lab = dm.log_prob(y, want_lp=True, want_proba=True, want_labels=True)
+    np.testing.assert_array_equal(lab, O.predict(y, t["means_y"], t["P"], w))
+    np.testing.assert_allclose(pr, O.predict_proba(y, t["means_y"], t["P"], w), rtol=1e-9, atol=1e-15)
     dm.close()
     big = np.eye(257)[None].astype(complex)
     with pytest.raises(NotImplementedError):

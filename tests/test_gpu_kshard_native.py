@@ -308,3 +308,29 @@ def test_host_transport_nonpd_raises_on_every_rank(sync):
     for rank, out in _run(_chol_worker, 2, (sync,)):
         for tag, msg, want in out:
             assert msg == want, (rank, tag, msg)
+
+
+def test_world1_rccl_double_buffered_snr_sweep(rccl1):
+    """Double-buffered tables (qce_kshard_set_spare): an SNR sweep of sync=False steps, each prepare filling the
+    table set the previous step did not read while that step runs; every step's h equals the single-GPU library
+    result at its own SNR (the reference's script loop, Bussgang_GMM.py:284-287, one estimate per SNR point)."""
+    import torch
+    from quantized_channel_estimation_amd import _lib
+    from quantized_channel_estimation_amd.sharding import ComponentShardEstimator
+    fx = load_model("fullmean")
+    y, _, N, A, n_bits, qtype, quantizer = case_args(fx, "b1_5")
+    yd = torch.from_numpy(np.ascontiguousarray(y)).cuda()
+    est = ComponentShardEstimator(fx["means_cplx"], fx["covs_cplx"], fx["weights"], 0, 1, device=0, comm=rccl1,
+                                  double_buffer=True)
+    single = _lib.DeviceModel(fx["means_cplx"], fx["covs_cplx"], fx["weights"], device=0)
+    snrs = [-10.0, 0.0, 5.0, 10.0, 20.0, -5.0]
+    outs = []
+    for snr in snrs:
+        est.prepare(None, snr, 1)
+        rows, h = est.estimate(yd, chunks=2, scatter=True, sync=False)
+        outs.append(h)  # each step writes its own output tensor
+    est.finish()
+    torch.cuda.synchronize()
+    for snr, h in zip(snrs, outs):
+        single.prepare(None, snr, 1)
+        assert rel_fro(h.cpu().numpy(), single.estimate(np.ascontiguousarray(y))) < 1e-12, snr

@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out/r04a
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-timeout -k 10 600 python -u -m pytest tests/test_gpu_kshard_native.py -x -v --timeout 170 --timeout-method thread > gpurun_out/r04a/pytest.log 2>&1 || { tail -40 gpurun_out/r04a/pytest.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_kshard_native.py tests/test_gpu_configs.py -x -v --timeout 170 --timeout-method thread > gpurun_out/r04a/pytest.log 2>&1 || { tail -40 gpurun_out/r04a/pytest.log; exit 1; }
 tail -3 gpurun_out/r04a/pytest.log
 timeout -k 10 300 python -u tools/kshard_native_step.py > gpurun_out/r04a/step.json 2> gpurun_out/r04a/step.err || { tail -30 gpurun_out/r04a/step.err; exit 1; }
 cat gpurun_out/r04a/step.json
