@@ -137,13 +137,16 @@ __global__ __launch_bounds__(256, 1) void k_wsum_f64(long long B, int M, int N, 
 
   // ring: chunk j of the stream order (chunk c outer, component k inner) -> slot j % NSLOT
   auto issue = [&](long long j) {
-    if (j >= nchunks) j = nchunks - 1;  // past the end: re-load the last chunk (never read), keeps vmcnt uniform
+    // the slot follows the unclamped stream index (past the end: the slot the barrier just freed, never read);
+    // only the source is clamped, to the last chunk, which keeps vmcnt uniform (a clamped slot index
+    // wrote into the last real chunk's slot while other waves could still read it)
+    char* dst = lds + (int)(j % G::NSLOT) * CHUNK + wave * 1024;
+    if (j >= nchunks) j = nchunks - 1;
     const long long st = j / G::NCH;
     const int cc = (int)(j % G::NCH);
     const long long c = st / K, k = st % K;
     const char* src = pack + ((((k * G::NMC + c) * G::NG + rg) * G::SLP + (long long)cc * G::CB) * 1024) +
                       wave * 1024 + lane * 16;
-    char* dst = lds + (int)(j % G::NSLOT) * CHUNK + wave * 1024;
 #pragma unroll
     for (int i = 0; i < G::LPW; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(src + i * NW * 1024),

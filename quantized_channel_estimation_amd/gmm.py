@@ -63,6 +63,28 @@ else:  # pragma: no cover
     _GaussianMixtureState = None
 
 
+def _owns_chain(a):
+    """True if every array in a's base chain is an ndarray and the last one owns its data (no foreign buffer that
+    could change behind a read-only view)."""
+    while isinstance(a, np.ndarray):
+        if a.base is None:
+            return a.flags.owndata
+        a = a.base
+    return isinstance(a, bytes)  # immutable Python buffer
+
+
+def _immutable(a):
+    """A read-only array whose data cannot change through another object: itself and every array of its base chain
+    read-only, the chain ending in memory it owns (a read-only view of a writable base can still change)."""
+    if not isinstance(a, np.ndarray) or not _owns_chain(a):
+        return False
+    while isinstance(a, np.ndarray):
+        if a.flags.writeable:
+            return False
+        a = a.base
+    return True
+
+
 def _fingerprint(*arrays):
     """Content key of the model parameters (in-place edits of means_cplx / covs_cplx / weights_
     invalidate the device model, as the reference re-reads them on every estimate_from_y)."""
@@ -301,7 +323,7 @@ class Gmm_nbit:
         (``freeze_params``) cannot change in place, so while the same read-only objects are attached the digest
         is reused instead of re-hashed."""
         arrs = (covs, means, w)
-        frozen = all(a is None or (isinstance(a, np.ndarray) and not a.flags.writeable) for a in arrs)
+        frozen = all(a is None or _immutable(a) for a in arrs)
         c = self.__dict__.get("_digest_cache")
         if frozen and c is not None and all(x is y for x, y in zip(c[0], arrs)):
             return c[1]
@@ -316,11 +338,14 @@ class Gmm_nbit:
         for name in ("means_cplx", "covs_cplx"):
             a = getattr(self, name, None)
             if isinstance(a, np.ndarray):
+                if a.base is not None:  # a view: its memory can still change elsewhere -- freeze a private copy
+                    a = a.copy()
+                    setattr(self, name, a)
                 a.flags.writeable = False
         wts = getattr(self.gm, "weights_", None)
         if isinstance(wts, np.ndarray):
-            if wts.dtype != np.float64:
-                self.gm.weights_ = wts = wts.astype(np.float64)
+            if wts.dtype != np.float64 or wts.base is not None:
+                self.gm.weights_ = wts = wts.astype(np.float64, copy=True)
             wts.flags.writeable = False
         return self
 
