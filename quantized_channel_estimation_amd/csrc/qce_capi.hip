@@ -133,9 +133,16 @@ bool want_f64(const qce_model* m) {
 // (m, s, acc) partial when h == nullptr (K-shard path)
 int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, double* oa,
             hipStream_t st, double* pk = nullptr, const double* shift = nullptr) {
-  const long long TS = qce_f64_tile(m->MP, m->NP);
+  int waves = 8;  // launch shape: 8 (default) / 4 / 42 (QCE_F64_WAVES), 42 only where the model's shape has it
+  {
+    const char* wv = getenv("QCE_F64_WAVES");
+    const int w = wv ? atoi(wv) : 8;
+    if (w == 4) waves = 4;
+    else if (w == 42 && qce_f64_dual(m->MP, m->NP, m->has_mean)) waves = 42;
+  }
+  const long long TS = qce_f64_tile(m->MP, m->NP, waves);
   const long long tiles = (B + TS - 1) / TS;
-  long long slots = m->cu_count;  // 128 KB of LDS: one workgroup per CU
+  long long slots = (long long)m->cu_count * (waves == 42 ? 2 : 1);  // LDS ring: one (two for 42) workgroups per CU
   const char* e = getenv("QCE_WORKGROUPS");
   if (e && atoll(e) > 0) slots = atoll(e);
   long long nwg, R, L;
@@ -175,17 +182,14 @@ int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om
   a.pa = m->fp_a.p;
   a.pk = pk;
   a.shift = shift;
-  {
-    const char* wv = getenv("QCE_F64_WAVES");  // 8 (default): two waves per SIMD where M, N <= 64
-    a.waves = (wv && atoi(wv) == 4) ? 4 : 8;
-  }
+  a.waves = waves;
 #ifdef QCE_STAMPS
   static unsigned long long* g_stamps = nullptr;
   if (!g_stamps) HIPCHK(hipMalloc(&g_stamps, sizeof(unsigned long long) * 4096 * 8 * 8));
   HIPCHK(hipMemsetAsync(g_stamps, 0, sizeof(unsigned long long) * 4096 * 8 * 8, st));
   a.stamps = nwg <= 4096 ? g_stamps : nullptr;
   g_f64_stamps = g_stamps;
-  g_f64_stamp_records = nwg * a.waves;
+  g_f64_stamp_records = nwg * (a.waves == 8 ? 8 : 4);
 #endif
   HIPCHK(qce_launch_est_f64(a, h == nullptr, st));
   return QCE_OK;

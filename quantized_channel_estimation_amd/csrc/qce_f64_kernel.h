@@ -38,15 +38,20 @@
 namespace {
 
 // Ring geometry: chunks of CB blocks (1 KB each), NSLOT chunks of LDS.  One barrier per chunk, so CB is as large
-// as the LDS allows (NSLOT >= 3, <= 144 KB) unless the per-component padding to whole chunks costs more load
-// traffic than the barriers it saves; CB is a multiple of 8 (whole pieces per wave for 4 and 8 waves).
+// as the LDS allows (NSLOT >= 3 within the LDS budget) unless the per-component padding to whole chunks costs more
+// load traffic than the barriers it saves; CB is a multiple of the scan step (whole pieces per wave).
+//   budget 144 KB: one workgroup per CU, CB in 16..48 step 8 (the layout k_pack_f64all packs: f64_bpc);
+//   budget  72 KB: two workgroups per CU (4 waves each, one per SIMD: the two waves of a SIMD come from different
+//                  workgroups, so one's barriers and ring waits are covered by the other's MFMAs), CB in 12..24 step 4
+//                  -- usable where it pads a component to the same BPC as the packed layout (f64_dual_ok).
 constexpr __host__ __device__ int f64_blocks(int MP, int NP, int hmi) {
   return (MP / 8) * (MP / 8 + 1) + hmi * (MP / 8) + (NP / 8) * (MP / 4 + hmi);
 }
-constexpr __host__ __device__ int f64_cb(int n) {
-  int best = 16;
+constexpr __host__ __device__ int f64_cb(int n, int budget = 144) {
+  const int lo = budget >= 144 ? 16 : 12, hi = budget >= 144 ? 48 : 24, step = budget >= 144 ? 8 : 4;
+  int best = lo;
   double best_cost = 1e30;
-  for (int cb = 16; cb <= 48; cb += 8) {
+  for (int cb = lo; cb <= hi; cb += step) {
     const int pad = (n + cb - 1) / cb * cb - n;
     const double cost = (double)pad / n + 2.0 / cb;
     if (cost < best_cost - 1e-12) {
@@ -56,10 +61,14 @@ constexpr __host__ __device__ int f64_cb(int n) {
   }
   return best;
 }
-constexpr __host__ __device__ int f64_nslot(int cb) { return 144 / cb < 8 ? 144 / cb : 8; }
-constexpr __host__ __device__ int f64_bpc(int n) { return (n + f64_cb(n) - 1) / f64_cb(n) * f64_cb(n); }
+constexpr __host__ __device__ int f64_nslot(int cb, int budget = 144) { return budget / cb < 8 ? budget / cb : 8; }
+constexpr __host__ __device__ int f64_bpc(int n, int budget = 144) {
+  return (n + f64_cb(n, budget) - 1) / f64_cb(n, budget) * f64_cb(n, budget);
+}
+// the two-workgroup ring reads the packed (144 KB) layout unchanged
+constexpr __host__ __device__ bool f64_dual_ok(int n) { return f64_bpc(n, 72) == f64_bpc(n, 144); }
 
-template <int MP, int NP, bool HM>
+template <int MP, int NP, bool HM, int BUD = 144>
 struct F64G {
   static constexpr int NTL = MP / 8;  // GL row tiles (16 real rows = 8 complex rows)
   static constexpr int NTW = NP / 8;  // GW row tiles
@@ -68,10 +77,10 @@ struct F64G {
   static constexpr int GL_BLOCKS = NTL * (NTL + 1) + HMI * NTL;
   static constexpr int GW_BLOCKS = NTW * (KP + HMI);
   static constexpr int BLOCKS = GL_BLOCKS + GW_BLOCKS;
-  static constexpr int CB = f64_cb(BLOCKS);  // blocks per ring chunk
-  static constexpr int NSLOT = f64_nslot(CB);
+  static constexpr int CB = f64_cb(BLOCKS, BUD);  // blocks per ring chunk
+  static constexpr int NSLOT = f64_nslot(CB, BUD);
   static constexpr int CHUNK = CB * 1024;
-  static constexpr int BPC = f64_bpc(BLOCKS);
+  static constexpr int BPC = f64_bpc(BLOCKS, BUD);
   static constexpr int CPC = BPC / CB;
   static_assert(BLOCKS == f64_blocks(MP, NP, HMI), "block count");
   static constexpr __host__ __device__ int gl_off(int T) { return T * (T + 1) + HMI * T; }
@@ -165,8 +174,8 @@ struct RingCursor {
 // ---------------------------------------------------------------------------
 // fused kernel
 // ---------------------------------------------------------------------------
-template <int MP, int NP, bool HM, int CT, int NW, bool OUT_PARTIAL>
-__global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int N, int K, int R, long long L,
+template <int MP, int NP, bool HM, int CT, int NW, bool OUT_PARTIAL, int BUD = 144>
+__global__ __launch_bounds__(NW * 64, BUD < 144 ? 2 : 1) void k_est_all_f64(long long B, int M, int N, int K, int R, long long L,
                                                          const double2* __restrict__ y, const char* __restrict__ pack,
                                                          const double* __restrict__ cconst, double2* __restrict__ h,
                                                          double* __restrict__ om, double* __restrict__ os,
@@ -174,7 +183,8 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
                                                          double* __restrict__ ps, double* __restrict__ pa,
                                                          double* __restrict__ pk, const double* __restrict__ shift,
                                                          unsigned long long* __restrict__ stamps) {
-  using G = F64G<MP, NP, HM>;
+  using G = F64G<MP, NP, HM, BUD>;
+  static_assert(G::BPC == F64G<MP, NP, HM>::BPC, "the ring must read the packed layout");
   constexpr int TS = NW * 16 * CT;           // samples per tile
   constexpr int LPW = G::CB / NW;  // global_load_lds per wave per chunk
   constexpr int E = 2;                        // boundary lead (blocks) = LDS prefetch distance
@@ -505,11 +515,26 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
 // or a 128-row output accumulator, take the registers of two 64-dim ones)
 constexpr int qce_f64_ct(int MP, int NP) { return (MP <= 64 && NP <= 64) ? 2 : 1; }
 
+// workgroup shape of the launch: 8 (one 8-wave workgroup per CU), 4 (one 4-wave workgroup, two column tiles per
+// wave) or 42 (two 4-wave workgroups per CU) -- 42 only where the two-workgroup ring reads the packed layout
+template <int MP, int NP, bool HM>
+constexpr bool qce_f64_dual_shape() {
+  return qce_f64_ct(MP, NP) == 2 && f64_dual_ok(F64G<MP, NP, HM>::BLOCKS);
+}
+
 template <int MP, int NP, bool HM, bool OP>
 hipError_t qce_f64_launch_t(const QceF64Args& a, hipStream_t st) {
   constexpr int CT0 = qce_f64_ct(MP, NP);
+  if constexpr (CT0 == 2 && f64_dual_ok(F64G<MP, NP, HM>::BLOCKS)) {
+    if (a.waves == 42) {  // two 4-wave workgroups per CU, one column tile per wave
+      hipLaunchKernelGGL((k_est_all_f64<MP, NP, HM, 1, 4, OP, 72>), dim3((unsigned)a.nwg), dim3(4 * 64), 0, st, a.B,
+                         a.M, a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa, a.pk,
+                         a.shift, a.stamps);
+      return hipGetLastError();
+    }
+  }
   if constexpr (CT0 == 2) {
-    if (a.waves == 8) {  // two waves per SIMD, one column tile each (same tile of 128 samples)
+    if (a.waves == 8 || a.waves == 42) {  // two waves per SIMD, one column tile each (same tile of 128 samples)
       hipLaunchKernelGGL((k_est_all_f64<MP, NP, HM, 1, 8, OP>), dim3((unsigned)a.nwg), dim3(8 * 64), 0, st, a.B, a.M,
                          a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa, a.pk,
                          a.shift, a.stamps);
