@@ -357,7 +357,7 @@ bool fft_enabled() {
 hipError_t detect_structure(qce_model* m) {
   const int K = m->K, N = m->N;
   m->fft_n1 = m->fft_n2 = 0;
-  if (!qce_fft_pow2(N) || N < 4 || qce_fft_tile(N, K) == 0 || K > 256) return hipSuccess;
+  if (N > 256 || !qce_fft_pow2(N) || N < 4 || qce_fft_tile(N, K) == 0 || K > 256) return hipSuccess;
   hipError_t e;
   if ((e = m->f_ceig.ensure((size_t)K * N)) != hipSuccess) return e;
   if ((e = m->f_col0.ensure((size_t)K * N)) != hipSuccess) return e;
@@ -499,7 +499,7 @@ int qce_model_create(int K, int N, const double* means_cplx, const double* covs_
   if (!out || !covs_cplx || !weights) return fail(QCE_EARG, "null argument");
   *out = nullptr;
   if (K <= 0 || N <= 0) return fail(QCE_EARG, "K and N must be positive");
-  if (pad_dim(N) < 0) return fail(QCE_ENOTIMPL, "N > 256 is not covered by the estimate kernels");
+  if (N > QCE_BIG_MAX) return fail(QCE_ENOTIMPL, "N > " + std::to_string(QCE_BIG_MAX) + " is not covered");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(QCE_EHIP, "no HIP device visible");
   if (device < 0 || device >= ndev) return fail(QCE_EARG, "device index out of range");
@@ -598,6 +598,8 @@ int qce_model_destroy(qce_model* m) {
   for (auto* b : {&m->fp_m, &m->fp_s, &m->fp_a, &m->part_a64, &m->fp_pack, &m->w64_scr, &m->shift_scr})
     b->release();
   m->WT.release();
+  m->big_ws.release();
+  m->big_d.release();
   for (auto* b : {&m->f_ceig, &m->f_rinvT, &m->f_cprime, &m->f_wT, &m->f_gain}) b->release();
   for (auto* b : {&m->f_col0, &m->f_mspec, &m->f_uT, &m->f_bT}) b->release();
   m->f_bad.release();
@@ -651,7 +653,7 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
   const int N = m->N, K = m->K;
   if (!A) M = N;
   if (M <= 0) return fail(QCE_EARG, "M must be positive");
-  if (pad_dim(M) < 0) return fail(QCE_ENOTIMPL, "M > 256 is not covered by the estimate kernels");
+  if (M > QCE_BIG_MAX) return fail(QCE_ENOTIMPL, "M > " + std::to_string(QCE_BIG_MAX) + " is not covered");
   int kind;
   int nb = 0;
   if (n_bits == 1.0) {
@@ -781,13 +783,15 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
   HIPCHK(m->status.ensure(K));
   HIPCHK(m->thr.ensure(256));
   HIPCHK(m->lab.ensure(256));
-  int MP = pad_dim(M), NP = pad_dim(N);
-  if (MP > 64 || NP > 64) {  // the chunk-streamed kernel family (qce_estimate_h2x.hip) starts at 64
+  m->big = (pad_dim(M) < 0 || pad_dim(N) < 0);
+  m->big_ws_valid = 0;
+  int MP = m->big ? 0 : pad_dim(M), NP = m->big ? 0 : pad_dim(N);
+  if (!m->big && (MP > 64 || NP > 64)) {  // the chunk-streamed kernel family (qce_estimate_h2x.hip) starts at 64
     MP = MP < 64 ? 64 : MP;
     NP = NP < 64 ? 64 : NP;
   }
-  const long long s32 = qce_pack_f32_stride(MP, NP, m->has_mean);
-  const long long s64 = qce_pack_f64_stride(MP, m->has_mean);
+  const long long s32 = m->big ? 0 : qce_pack_f32_stride(MP, NP, m->has_mean);
+  const long long s64 = m->big ? 0 : qce_pack_f64_stride(MP, m->has_mean);
   HIPCHK(m->pack32.ensure((size_t)s32 * K));
   HIPCHK(m->pack64.ensure((size_t)s64 * K));
   int identityA = 0;
@@ -866,9 +870,11 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
   p.pack32 = nullptr;  // selective-mode / log-prob tables are packed on first use (ensure_packs)
   p.pack64 = nullptr;
   HIPCHK(qce_launch_prepare(p, st));
-  m->f64_active = want_f64(m) && qce_f64_shape(MP, NP);
-  m->f64_wide = want_f64(m) && !m->f64_active && qce_wsum_shape(MP, NP);
-  if (m->f64_wide) {
+  m->f64_active = !m->big && want_f64(m) && qce_f64_shape(MP, NP);
+  m->f64_wide = !m->big && want_f64(m) && !m->f64_active && qce_wsum_shape(MP, NP);
+  if (m->big) {
+    // GEMM-based FP64 path (qce_big.hip): the dense tables are all it reads; the stacked filters on first use
+  } else if (m->f64_wide) {
     // FP64 filter tables of the two-pass path; the log-prob table is packed on first use (ensure_pack64)
     HIPCHK(m->pack_ws.ensure((size_t)qce_pack_wsum_bytes(MP, NP, m->has_mean) * K));
     HIPCHK(qce_launch_pack_wsum(K, M, N, MP, NP, m->has_mean, m->W.p, m->bvec.p,
@@ -1033,7 +1039,7 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
   if (rc) return rc;
   if (B < 0 || (B > 0 && (!y || !h_out))) return fail(QCE_EARG, "bad y / h_out");
   if (B == 0) return QCE_OK;
-  if (!m->fft_active && mode != QCE_MODE_ALL && !qce_select_shape_supported(m->MP, m->NP))
+  if (!m->fft_active && !m->big && mode != QCE_MODE_ALL && !qce_select_shape_supported(m->MP, m->NP))
     return fail(QCE_ENOTIMPL, "selective modes: shape not covered");
   if (mode != QCE_MODE_ALL && m->K > qce_select_max_k())
     return fail(QCE_ENOTIMPL, "selective modes support K <= " + std::to_string(qce_select_max_k()));
@@ -1048,6 +1054,33 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
   if (io == QCE_IO_HOST) {
     HIPCHK(m->h_scr.ensure((size_t)B * m->N));
     dh = m->h_scr.p;
+  }
+  if (m->big) {  // N or M beyond 256: lp GEMM -> FP64 weights -> stacked-filter GEMM (qce_big.hip)
+    int kmode = 0, n = 0;
+    double p = 0.0;
+    if (mode == QCE_MODE_TOPN) {
+      if (mode_param < 1.0 || mode_param != floor(mode_param)) return fail(QCE_EARG, "top-n needs an integer n >= 1");
+      n = mode_param > 1e9 ? 1000000000 : (int)mode_param;
+      kmode = (n == 1) ? 3 : 1;
+    } else if (mode == QCE_MODE_CUMP) {
+      kmode = 2;
+      p = mode_param;
+    } else if (mode != QCE_MODE_ALL) {
+      return fail(QCE_EARG, "unknown mode");
+    }
+    HIPCHK(m->lp_scr.ensure((size_t)B * m->K));
+    HIPCHK(m->w64_scr.ensure((size_t)B * m->K));
+    if ((rc = qce_big_lp(m, dy, B, m->lp_scr.p, st))) return rc;
+    if (mode == QCE_MODE_ALL)  // responsibilities = proba (:220-228: no renormalisation)
+      HIPCHK(qce_launch_select(B, m->K, m->lp_scr.p, 0, 0, 0.0, m->w64_scr.p, nullptr, nullptr, st));
+    else
+      HIPCHK(qce_launch_select(B, m->K, m->lp_scr.p, kmode, n, p, nullptr, nullptr, nullptr, st, m->w64_scr.p));
+    if ((rc = qce_big_wsum(m, dy, B, m->w64_scr.p, dh, m->N, st))) return rc;
+    if (io == QCE_IO_HOST) {
+      HIPCHK(hipMemcpyAsync(h_out, dh, sizeof(double2) * (size_t)B * m->N, hipMemcpyDeviceToHost, st));
+      HOST_SYNC_CHECK(m, st);
+    }
+    return QCE_OK;
   }
   if (!m->fft_active && (mode != QCE_MODE_ALL || !use_h2()) && (rc = ensure_packs(m, st))) return rc;
   QceEstArgs a = est_args(m, dy, B);
@@ -1136,7 +1169,7 @@ int qce_log_prob(qce_model* m, const double* X, int64_t B, double* lp_out, doubl
   hipStream_t st = pick_stream(m, stream);
   const double2* dx = nullptr;
   if ((rc = stage_input(m, X, B, io, st, &dx))) return rc;
-  if (!m->fft_active && (rc = ensure_packs(m, st))) return rc;
+  if (!m->fft_active && !m->big && (rc = ensure_packs(m, st))) return rc;
   QceEstArgs a = est_args(m, dx, B);
   const size_t BK = (size_t)B * m->K;
   double* dlp = lp_out;
@@ -1158,6 +1191,8 @@ int qce_log_prob(qce_model* m, const double* X, int64_t B, double* lp_out, doubl
     QceFftEstArgs fa = fft_args(m, dx, B);
     fa.lp = dlp;
     HIPCHK(qce_launch_fft_est(fa, 1, st));
+  } else if (m->big) {
+    if ((rc = qce_big_lp(m, dx, B, dlp, st))) return rc;
   } else {
     HIPCHK(qce_launch_lp(a, dlp, st));
   }
@@ -1198,9 +1233,11 @@ int qce_estimate_partial(qce_model* m, const double* y, int64_t B, double* m_out
     fa.oa = da;
     if (m->fft_mfma) HIPCHK(qce_launch_fft_mfma(fa, 3, st));
     else HIPCHK(qce_launch_fft_est(fa, 3, st));
-  } else if (m->f64_active || m->f64_wide) {  // FP64 partial, rounded to the f32 accumulator of this entry point
+  } else if (m->f64_active || m->f64_wide || m->big) {  // FP64 partial, rounded to this entry point's f32 accumulator
     HIPCHK(m->part_a64.ensure((size_t)B * 2 * m->N));
-    if (m->f64_active) {
+    if (m->big) {
+      if ((rc = qce_big_partial(m, dy, B, 1, dm, ds, m->part_a64.p, nullptr, nullptr, st))) return rc;
+    } else if (m->f64_active) {
       if ((rc = run_f64(m, dy, B, nullptr, dm, ds, m->part_a64.p, st))) return rc;
     } else if ((rc = run_wide(m, dy, B, 1, nullptr, dm, ds, m->part_a64.p, nullptr, nullptr, st))) {
       return rc;
@@ -1241,7 +1278,9 @@ int qce_estimate_partial_f64(qce_model* m, const double* y, int64_t B, double* m
     ds = m->s_scr.p;
     da = m->part_a64.p;
   }
-  if (!m->fft_active && m->f64_active) {
+  if (!m->fft_active && m->big) {
+    if ((rc = qce_big_partial(m, dy, B, 1, dm, ds, da, nullptr, nullptr, st))) return rc;
+  } else if (!m->fft_active && m->f64_active) {
     if ((rc = run_f64(m, dy, B, nullptr, dm, ds, da, st))) return rc;
   } else if (!m->fft_active && m->f64_wide) {
     if ((rc = run_wide(m, dy, B, 1, nullptr, dm, ds, da, nullptr, nullptr, st))) return rc;
@@ -1288,7 +1327,9 @@ int qce_estimate_partial_shifted(qce_model* m, const double* y, int64_t B, const
     HIPCHK(hipMemcpyAsync(m->shift_scr.p, shift, sizeof(double), hipMemcpyHostToDevice, st));
     dshift = m->shift_scr.p;
   }
-  if (!m->fft_active && m->f64_active) {
+  if (!m->fft_active && m->big) {
+    if ((rc = qce_big_partial(m, dy, B, 2, nullptr, nullptr, nullptr, dp, dshift, st))) return rc;
+  } else if (!m->fft_active && m->f64_active) {
     if ((rc = run_f64(m, dy, B, nullptr, nullptr, nullptr, nullptr, st, dp, dshift))) return rc;
   } else if (!m->fft_active && m->f64_wide) {
     if ((rc = run_wide(m, dy, B, 2, nullptr, nullptr, nullptr, nullptr, dp, dshift, st))) return rc;
@@ -1514,6 +1555,8 @@ int qce_em_estep(qce_model* m, const double* X, int64_t B, double* resp_out, dou
     QceFftEstArgs fa = fft_args(m, dx, B);
     fa.lp = dlp;
     HIPCHK(qce_launch_fft_est(fa, 1, st));
+  } else if (m->big) {
+    if ((rc = qce_big_lp(m, dx, B, dlp, st))) return rc;
   } else {
     if ((rc = ensure_packs(m, st))) return rc;
     QceEstArgs a = est_args(m, dx, B);
@@ -1643,6 +1686,7 @@ static int assigned_impl(qce_model* m, const double* y, int64_t B, const int64_t
   if (B < 0 || (B > 0 && (!y || !h_out))) return fail(QCE_EARG, "bad arguments");
   if (!comp && B > m->K) return fail(QCE_EARG, "without comp, sample b uses component b: B <= K");
   if (B == 0) return QCE_OK;
+  if (m->big) return fail(QCE_ENOTIMPL, "per-sample filters / LS cover N, M <= 256");
   if ((rc = ensure_dense(m))) return rc;
   DeviceGuard g(m->device);
   hipStream_t st = pick_stream(m, stream);
@@ -1883,6 +1927,7 @@ int qce_weighted_estimate(qce_model* m, const double2* y, long long B, const dou
     HIPCHK(qce_launch_fft_est(fa, 2, st));
     return QCE_OK;
   }
+  if (m->big) return qce_big_wsum(m, y, B, w, h, m->N, st);
   HIPCHK(m->WT.ensure((size_t)m->K * m->M * m->N));
   HIPCHK(qce_launch_sparse_f64(B, m->N, m->M, m->K, y, w, m->W.p, m->bvec.p, m->WT.p, !m->wt_valid, h, st));
   m->wt_valid = 1;

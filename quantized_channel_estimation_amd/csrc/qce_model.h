@@ -78,6 +78,10 @@ struct qce_model {
   DevBuf<double2> WT;       // transposed filters W_k^T for the FP64 selective-mode kernel (built lazily)
   int wt_valid = 0;
   int cu_count = 256;
+  // dimensions beyond the fused kernels' 256 (qce_big.hip): GEMM-based FP64 path
+  int big = 0;
+  DevBuf<double2> big_ws, big_d;  // stacked transposed filters (N x K x M); per-chunk intermediate
+  int big_ws_valid = 0;
   // Fourier-domain path for (block-)circulant mixtures (qce_fft.hip): structure found at creation
   int fft_n1 = 0, fft_n2 = 0;
   int fft_active = 0;   // the last prepare took the Fourier path (dense tables computed lazily)
@@ -108,3 +112,11 @@ struct qce_model {
 int qce_set_error(int code, const std::string& msg);  // sets qce_last_error() and returns code
 // h_b = sum_k w[b][k] (W_k y_b + b_k), w (B x K) FP64 selection weights on the device (dense or Fourier path)
 int qce_weighted_estimate(qce_model* m, const double2* y, long long B, const double* w, double2* h, hipStream_t st);
+
+// qce_big.hip: the GEMM-based FP64 path for N or M in (256, QCE_BIG_MAX]
+#define QCE_BIG_MAX 4096
+int qce_big_lp(qce_model* m, const double2* y, long long B, double* lp, hipStream_t st);
+int qce_big_wsum(qce_model* m, const double2* y, long long B, const double* w, double2* out, long long ldo,
+                 hipStream_t st);
+int qce_big_partial(qce_model* m, const double2* y, long long B, int wmode, double* om, double* os, double* oa,
+                    double* pk, const double* shift, hipStream_t st);

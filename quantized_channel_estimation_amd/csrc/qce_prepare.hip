@@ -242,7 +242,9 @@ __global__ __launch_bounds__(256) void k_gain_cr(int M, int N, const double2* __
   const double2* cy = Cy + (long long)k * M * M;
   double2* cr = Cr + (long long)k * M * M;
   double* gout = gain + (long long)k * M;
-  __shared__ double g[256], pinv[256];
+  extern __shared__ double gain_lds[];  // 2 M doubles: the gains and diag(Cy)^-1/2 (any M)
+  double* g = gain_lds;
+  double* pinv = gain_lds + M;
   __shared__ double s_beta;
   const double PI = 3.14159265358979323846;
   for (int i = tid; i < M; i += 256) {
@@ -777,7 +779,7 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // row slices per component: 4 where the gains are cheap to derive in every slice (1 bit, infinite resolution)
   const unsigned gslices = (p.kind == 0 || p.kind == 2) ? 4u : 1u;
-  hipLaunchKernelGGL(k_gain_cr, dim3(K, gslices), dim3(256), 0, st, M, N, p.Cy, p.Cr, p.gain, p.A, p.means, p.means_y, p.Aeff,
+  hipLaunchKernelGGL(k_gain_cr, dim3(K, gslices), dim3(256), (size_t)2 * M * sizeof(double), st, M, N, p.Cy, p.Cr, p.gain, p.A, p.means, p.means_y, p.Aeff,
                      p.kind, p.n_bits, p.quant_kind, p.delta, p.thr, p.lab, p.beta_first);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // M <= 64: QCE_CHOL = lds (default) | tri | wave picks the factorisation kernel (A/B runs; metric config,

@@ -155,7 +155,7 @@ def test_bench_kshard_two_ranks_gloo_one_gpu():
 def test_wide_k_all_modes(K):
     """K beyond one wave's 256 components: 'all', argmax, top-3, cumulative-p 0.9, predict_proba and the labels
     (k_select_wide: the row in LDS, a bitonic sort of (proba, index)) against the FP64 oracle
-    (gmm_cplx_bussgang.py:197-243, :335-367); N > 256 stays refused at model creation."""
+    (gmm_cplx_bussgang.py:197-243, :335-367)."""
     from oracle import qce_oracle as O
     from quantized_channel_estimation_amd import _lib, inputs
     means, covs, w = inputs.synthetic_model(K, 16, seed=9)
@@ -172,6 +172,43 @@ def test_wide_k_all_modes(K):
     np.testing.assert_array_equal(lab, O.predict(y, t["means_y"], t["P"], w))
     np.testing.assert_allclose(pr, O.predict_proba(y, t["means_y"], t["P"], w), rtol=1e-9, atol=1e-15)
     dm.close()
-    big = np.eye(257)[None].astype(complex)
-    with pytest.raises(NotImplementedError):
-        _lib.DeviceModel(None, big, np.ones(1))
+
+
+@pytest.mark.parametrize("N,pilots,K,with_mean", [(320, 1, 6, False), (288, 1, 5, True), (136, 2, 4, False)])
+def test_wide_dimensions_all_modes(N, pilots, K, with_mean):
+    """Channel / observation dimensions beyond 256 (the GEMM-based FP64 path, qce_big.hip): N = 320 and 288 (with
+    means) with A = I, and N = 136 with 2 pilots (M = 272, a general A): 'all', argmax, top-3, cumulative-p 0.9 and
+    predict_proba against the FP64 oracle at 1e-9; the reference runs any N (gmm_cplx_bussgang.py:197-243)."""
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import _lib, inputs
+    means, covs, w = inputs.synthetic_model(K, N, seed=3)
+    rng = np.random.default_rng(4)
+    if with_mean:
+        means = 0.3 * (rng.standard_normal((K, N)) + 1j * rng.standard_normal((K, N)))
+    M = N * pilots
+    A = None if pilots == 1 else np.kron(np.exp(2j * np.pi * rng.random((pilots, 1))), np.eye(N)) / np.sqrt(pilots)
+    y = (np.sign(rng.standard_normal((48, M))) + 1j * np.sign(rng.standard_normal((48, M)))) / np.sqrt(2)
+    dm = _lib.DeviceModel(means, covs, w)
+    dm.prepare(A, 5.0, 1.0)
+    Ao = np.eye(N) if A is None else A
+    tol = 1e-9 if pilots == 1 else 1e-6  # 1 bit with a general A: the arcsine law's documented sensitivity
+    for mode, (cm, param) in (("all", (_lib.MODE_ALL, 0.0)), (1, (_lib.MODE_TOPN, 1.0)), (3, (_lib.MODE_TOPN, 3.0)),
+                              (0.9, (_lib.MODE_CUMP, 0.9))):
+        h = dm.estimate(y, cm, param)
+        ho = O.estimate(means, covs, w, y, 5.0, N, Ao, mode, 1)
+        assert rel_fro(h, ho) < tol, (mode, rel_fro(h, ho))
+    t = O.prepare(means, covs, Ao, 5.0, 1)
+    _, pr, lab = dm.log_prob(y, want_lp=False, want_proba=True, want_labels=True)
+    np.testing.assert_array_equal(lab, O.predict(y, t["means_y"], t["P"], w))
+    np.testing.assert_allclose(pr, O.predict_proba(y, t["means_y"], t["P"], w), rtol=1e-6, atol=1e-12)
+    # the K-shard partial of this path recombines to the same estimate
+    m_, s_, a_ = dm.partial64(y)
+    from quantized_channel_estimation_amd.sharding import combine_partials_numpy
+    hp = combine_partials_numpy([(m_, s_, a_)], N)
+    assert rel_fro(hp, O.estimate(means, covs, w, y, 5.0, N, Ao, "all", 1)) < tol
+    dm.close()
+    import ctypes
+    h = ctypes.c_void_p()
+    one = np.ones(2)
+    with pytest.raises(NotImplementedError):  # beyond QCE_BIG_MAX: refused before any upload
+        _lib.check(_lib.load().qce_model_create(1, 4097, None, _lib.ptr(one), _lib.ptr(one), 0, ctypes.byref(h)))

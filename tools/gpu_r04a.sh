@@ -8,6 +8,12 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_kshard_native.py tests/test
 tail -3 gpurun_out/r04a/pytest.log
 timeout -k 10 300 python -u tools/kshard_native_step.py > gpurun_out/r04a/step.json 2> gpurun_out/r04a/step.err || { tail -30 gpurun_out/r04a/step.err; exit 1; }
 cat gpurun_out/r04a/step.json
+# one rank's share of the 8-GPU metric step (K/N = 16 components over the whole batch), 1 and 2 chunks, with and
+# without the spare table set (the next prepare overlapping the current step)
+for C in 1 2; do for SB in "" "--single-buffer"; do
+  timeout -k 10 200 python -u tools/kshard_native_step.py --K 16 --chunks $C --steps 20 $SB >> gpurun_out/r04a/rank16.jsonl 2>> gpurun_out/r04a/rank16.err || { tail -20 gpurun_out/r04a/rank16.err; exit 1; }
+done; done
+cat gpurun_out/r04a/rank16.jsonl
 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun_out/r04a/prof -o trace -- python3 tools/kshard_native_step.py --steps 5 > gpurun_out/r04a/prof.log 2> gpurun_out/r04a/prof.err || { tail -30 gpurun_out/r04a/prof.err; exit 1; }
 find gpurun_out/r04a/prof -name "*kernel_stats.csv" | head -3
 timeout -k 10 60 ./tools/probe/mfma_f64_probe > gpurun_out/r04a/mfma_f64_probe.txt 2>&1 || true
