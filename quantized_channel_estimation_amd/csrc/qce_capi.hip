@@ -183,6 +183,10 @@ int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om
   a.pk = pk;
   a.shift = shift;
   a.waves = waves;
+  {
+    const char* pv = getenv("QCE_F64_PIPE");  // A/B switch of the issue order
+    a.pipe = (pv && pv[0] == '1') ? 1 : 0;
+  }
 #ifdef QCE_STAMPS
   static unsigned long long* g_stamps = nullptr;
   if (!g_stamps) HIPCHK(hipMalloc(&g_stamps, sizeof(unsigned long long) * 4096 * 8 * 8));

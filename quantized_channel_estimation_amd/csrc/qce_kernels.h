@@ -102,6 +102,7 @@ struct QceF64Args {
   double* pk = nullptr;   // shifted packed partial B x (2N+2): [s e^{m-shift}, 0, acc e^{m-shift}] (instead of om/os/oa)
   const double* shift = nullptr;  // device pointer: the shared shift M* of the packed partial
   unsigned long long* stamps = nullptr;  // diagnostic builds (-DQCE_STAMPS): per-wave segment cycles
+  int pipe = 0;   // deferred-half MFMA issue order (QCE_F64_PIPE=1)
   int waves = 8;  // workgroup shape where M, N <= 64: 8 waves x 1 column tile (two per SIMD), 4 x 2 (QCE_F64_WAVES=4),
                   // or 42: two 4-wave workgroups per CU (QCE_F64_WAVES=42)
 };

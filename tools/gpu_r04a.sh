@@ -18,3 +18,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d gpurun
 find gpurun_out/r04a/prof -name "*kernel_stats.csv" | head -3
 timeout -k 10 60 ./tools/probe/mfma_f64_probe > gpurun_out/r04a/mfma_f64_probe.txt 2>&1 || true
 cat gpurun_out/r04a/mfma_f64_probe.txt
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 120 rocprofv3 -L > gpurun_out/r04a/counters_list.txt 2>&1 || true
+grep -i -E "DRAM|MALL|EA0_RD|EA_RD|HBM" gpurun_out/r04a/counters_list.txt | head -40
