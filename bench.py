@@ -601,6 +601,8 @@ def main():
     roofline = roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic)
     if traffic is not None:
         roofline["traffic_source"] = os.path.relpath(tpath, ROOT) + " (rocprofv3 PMC of this build)"
+        if tj.get("dram"):
+            roofline["traffic_dram"] = tj["dram"].get("bytes_per_launch")
     elif traffic_note:
         roofline["traffic_note"] = traffic_note
 

@@ -133,16 +133,9 @@ bool want_f64(const qce_model* m) {
 // (m, s, acc) partial when h == nullptr (K-shard path)
 int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, double* oa,
             hipStream_t st, double* pk = nullptr, const double* shift = nullptr) {
-  int waves = 8;  // launch shape: 8 (default) / 4 / 42 (QCE_F64_WAVES), 42 only where the model's shape has it
-  {
-    const char* wv = getenv("QCE_F64_WAVES");
-    const int w = wv ? atoi(wv) : 8;
-    if (w == 4) waves = 4;
-    else if (w == 42 && qce_f64_dual(m->MP, m->NP, m->has_mean)) waves = 42;
-  }
-  const long long TS = qce_f64_tile(m->MP, m->NP, waves);
+  const long long TS = qce_f64_tile(m->MP, m->NP);
   const long long tiles = (B + TS - 1) / TS;
-  long long slots = (long long)m->cu_count * (waves == 42 ? 2 : 1);  // LDS ring: one (two for 42) workgroups per CU
+  long long slots = m->cu_count;  // 128 KB of LDS: one workgroup per CU
   const char* e = getenv("QCE_WORKGROUPS");
   if (e && atoll(e) > 0) slots = atoll(e);
   long long nwg, R, L;
@@ -182,10 +175,9 @@ int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om
   a.pa = m->fp_a.p;
   a.pk = pk;
   a.shift = shift;
-  a.waves = waves;
   {
-    const char* pv = getenv("QCE_F64_PIPE");  // A/B switch of the issue order
-    a.pipe = (pv && pv[0] == '1') ? 1 : 0;
+    const char* wv = getenv("QCE_F64_WAVES");  // 8 (default): two waves per SIMD where M, N <= 64
+    a.waves = (wv && atoi(wv) == 4) ? 4 : 8;
   }
 #ifdef QCE_STAMPS
   static unsigned long long* g_stamps = nullptr;
@@ -193,7 +185,7 @@ int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om
   HIPCHK(hipMemsetAsync(g_stamps, 0, sizeof(unsigned long long) * 4096 * 8 * 8, st));
   a.stamps = nwg <= 4096 ? g_stamps : nullptr;
   g_f64_stamps = g_stamps;
-  g_f64_stamp_records = nwg * (a.waves == 8 ? 8 : 4);
+  g_f64_stamp_records = nwg * a.waves;
 #endif
   HIPCHK(qce_launch_est_f64(a, h == nullptr, st));
   return QCE_OK;

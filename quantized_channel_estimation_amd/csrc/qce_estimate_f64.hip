@@ -161,20 +161,14 @@ __global__ __launch_bounds__(64) void k_pack_f64all(int M, int N, int MP, int NP
 // host side
 // ---------------------------------------------------------------------------
 namespace {
-int blocks_per_comp(int MP, int NP, int hm) { return f64_bpc(f64_blocks(MP, NP, hm ? 1 : 0)); }
+int blocks_per_comp(int MP, int NP, int hm) { return f64_bpc(f64_blocks(MP, NP, hm ? 1 : 0), f64_minlead(MP, NP)); }
 }  // namespace
 
 bool qce_f64_shape(int MP, int NP) {
   auto ok = [](int v) { return v == 16 || v == 32 || v == 64 || v == 128; };
   return ok(MP) && ok(NP);
 }
-bool qce_f64_dual(int MP, int NP, int has_mean) {
-  return MP <= 64 && NP <= 64 && f64_dual_ok(f64_blocks(MP, NP, has_mean ? 1 : 0));
-}
-int qce_f64_tile(int MP, int NP, int waves) {
-  if (waves == 42 && MP <= 64 && NP <= 64) return 4 * 16;  // 4 waves x 1 column tile
-  return 4 * 16 * ((MP <= 64 && NP <= 64) ? 2 : 1);
-}
+int qce_f64_tile(int MP, int NP) { return 4 * 16 * ((MP <= 64 && NP <= 64) ? 2 : 1); }
 long long qce_pack_f64all_bytes(int MP, int NP, int has_mean) { return (long long)blocks_per_comp(MP, NP, has_mean) * 1024; }
 
 hipError_t qce_launch_pack_f64all(int K, int M, int N, int MP, int NP, int has_mean, const double2* Linv,
@@ -199,7 +193,7 @@ hipError_t qce_launch_est_f64(const QceF64Args& a, bool out_partial, hipStream_t
     default: e = hipErrorInvalidValue;
   }
   if (e != hipSuccess) return e;
-  const long long TS = qce_f64_tile(a.MP, a.NP, a.waves);
+  const long long TS = qce_f64_tile(a.MP, a.NP);
   const long long tiles = (a.B + TS - 1) / TS;
   const long long tail0 = (long long)a.R * a.nwg;
   if (a.L > 0 && tiles > tail0) {  // some tail tile may be cut between workgroups

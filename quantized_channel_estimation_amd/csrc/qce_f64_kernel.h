@@ -38,20 +38,21 @@
 namespace {
 
 // Ring geometry: chunks of CB blocks (1 KB each), NSLOT chunks of LDS.  One barrier per chunk, so CB is as large
-// as the LDS allows (NSLOT >= 3 within the LDS budget) unless the per-component padding to whole chunks costs more
-// load traffic than the barriers it saves; CB is a multiple of the scan step (whole pieces per wave).
-//   budget 144 KB: one workgroup per CU, CB in 16..48 step 8 (the layout k_pack_f64all packs: f64_bpc);
-//   budget  72 KB: two workgroups per CU (4 waves each, one per SIMD: the two waves of a SIMD come from different
-//                  workgroups, so one's barriers and ring waits are covered by the other's MFMAs), CB in 12..24 step 4
-//                  -- usable where it pads a component to the same BPC as the packed layout (f64_dual_ok).
+// as the LDS allows (NSLOT >= 3, <= 144 KB) unless the per-component padding to whole chunks costs more load
+// traffic than the barriers it saves; CB is a multiple of 8 (whole pieces per wave for 4 and 8 waves).
 constexpr __host__ __device__ int f64_blocks(int MP, int NP, int hmi) {
   return (MP / 8) * (MP / 8 + 1) + hmi * (MP / 8) + (NP / 8) * (MP / 4 + hmi);
 }
-constexpr __host__ __device__ int f64_cb(int n, int budget = 144) {
-  const int lo = budget >= 144 ? 16 : 12, hi = budget >= 144 ? 48 : 24, step = budget >= 144 ? 8 : 4;
-  int best = lo;
+// minlead: blocks of prefetch lead the ring must keep ((NSLOT - 2) chunks are in flight while one is read).  The
+// shapes with a padded dimension of 128 run one wave per SIMD (their registers), where no second wave covers a ring
+// wait: they keep >= 96 blocks (~12k MFMA cycles) in flight; the 2-waves-per-SIMD shapes take the cheapest layout.
+constexpr __host__ __device__ int f64_minlead(int MP, int NP) { return (MP >= 128 || NP >= 128) ? 96 : 0; }
+constexpr __host__ __device__ int f64_nslot(int cb) { return 144 / cb < 8 ? 144 / cb : 8; }
+constexpr __host__ __device__ int f64_cb(int n, int minlead = 0) {
+  int best = 16;
   double best_cost = 1e30;
-  for (int cb = lo; cb <= hi; cb += step) {
+  for (int cb = 16; cb <= 48; cb += 8) {
+    if ((f64_nslot(cb) - 2) * cb < minlead) continue;
     const int pad = (n + cb - 1) / cb * cb - n;
     const double cost = (double)pad / n + 2.0 / cb;
     if (cost < best_cost - 1e-12) {
@@ -61,14 +62,11 @@ constexpr __host__ __device__ int f64_cb(int n, int budget = 144) {
   }
   return best;
 }
-constexpr __host__ __device__ int f64_nslot(int cb, int budget = 144) { return budget / cb < 8 ? budget / cb : 8; }
-constexpr __host__ __device__ int f64_bpc(int n, int budget = 144) {
-  return (n + f64_cb(n, budget) - 1) / f64_cb(n, budget) * f64_cb(n, budget);
+constexpr __host__ __device__ int f64_bpc(int n, int minlead = 0) {
+  return (n + f64_cb(n, minlead) - 1) / f64_cb(n, minlead) * f64_cb(n, minlead);
 }
-// the two-workgroup ring reads the packed (144 KB) layout unchanged
-constexpr __host__ __device__ bool f64_dual_ok(int n) { return f64_bpc(n, 72) == f64_bpc(n, 144); }
 
-template <int MP, int NP, bool HM, int BUD = 144>
+template <int MP, int NP, bool HM>
 struct F64G {
   static constexpr int NTL = MP / 8;  // GL row tiles (16 real rows = 8 complex rows)
   static constexpr int NTW = NP / 8;  // GW row tiles
@@ -77,10 +75,10 @@ struct F64G {
   static constexpr int GL_BLOCKS = NTL * (NTL + 1) + HMI * NTL;
   static constexpr int GW_BLOCKS = NTW * (KP + HMI);
   static constexpr int BLOCKS = GL_BLOCKS + GW_BLOCKS;
-  static constexpr int CB = f64_cb(BLOCKS, BUD);  // blocks per ring chunk
-  static constexpr int NSLOT = f64_nslot(CB, BUD);
+  static constexpr int CB = f64_cb(BLOCKS, f64_minlead(MP, NP));  // blocks per ring chunk
+  static constexpr int NSLOT = f64_nslot(CB);
   static constexpr int CHUNK = CB * 1024;
-  static constexpr int BPC = f64_bpc(BLOCKS, BUD);
+  static constexpr int BPC = f64_bpc(BLOCKS, f64_minlead(MP, NP));
   static constexpr int CPC = BPC / CB;
   static_assert(BLOCKS == f64_blocks(MP, NP, HMI), "block count");
   static constexpr __host__ __device__ int gl_off(int T) { return T * (T + 1) + HMI * T; }
@@ -174,8 +172,8 @@ struct RingCursor {
 // ---------------------------------------------------------------------------
 // fused kernel
 // ---------------------------------------------------------------------------
-template <int MP, int NP, bool HM, int CT, int NW, bool OUT_PARTIAL, int BUD = 144, bool PIPE = false>
-__global__ __launch_bounds__(NW * 64, BUD < 144 ? 2 : 1) void k_est_all_f64(long long B, int M, int N, int K, int R, long long L,
+template <int MP, int NP, bool HM, int CT, int NW, bool OUT_PARTIAL>
+__global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int N, int K, int R, long long L,
                                                          const double2* __restrict__ y, const char* __restrict__ pack,
                                                          const double* __restrict__ cconst, double2* __restrict__ h,
                                                          double* __restrict__ om, double* __restrict__ os,
@@ -183,8 +181,7 @@ __global__ __launch_bounds__(NW * 64, BUD < 144 ? 2 : 1) void k_est_all_f64(long
                                                          double* __restrict__ ps, double* __restrict__ pa,
                                                          double* __restrict__ pk, const double* __restrict__ shift,
                                                          unsigned long long* __restrict__ stamps) {
-  using G = F64G<MP, NP, HM, BUD>;
-  static_assert(G::BPC == F64G<MP, NP, HM>::BPC, "the ring must read the packed layout");
+  using G = F64G<MP, NP, HM>;
   constexpr int TS = NW * 16 * CT;           // samples per tile
   constexpr int LPW = G::CB / NW;  // global_load_lds per wave per chunk
   constexpr int E = 2;                        // boundary lead (blocks) = LDS prefetch distance
@@ -303,7 +300,6 @@ __global__ __launch_bounds__(NW * 64, BUD < 144 ? 2 : 1) void k_est_all_f64(long
       int rslot = slot0;
       int roff = lane * 16 + rslot * G::CHUNK;
       auto rd = [&](int off) -> double2 { return *reinterpret_cast<const double2*>(&lds[roff + off]); };
-      if constexpr (!PIPE) {
       f64x4 acc[CT], accp[CT];
       double qp[CT], p[CT];
       double bs0[CT], bs1[CT];
@@ -455,186 +451,6 @@ __global__ __launch_bounds__(NW * 64, BUD < 144 ? 2 : 1) void k_est_all_f64(long
             }
           },
           std::make_integer_sequence<int, G::BPC>{});
-      } else {
-        // Software-pipelined issue (PIPE): the second MFMA half (a.y) of each data block is deferred to the next
-        // block's step, so consecutive MFMAs never share an accumulator (one wave per SIMD at N = 128 cannot hide
-        // a dependent MFMA's latency behind another wave).  GL splits the halves over AX / AY (the tile's
-        // L^-1 y = AX + AY), one set per tile parity so a tile's deferred last half and the next tile's first
-        // MFMAs do not collide; the tile is folded one step after its last half was issued.  GW's halves
-        // interleave over the row tiles (out[T] receives its two halves three MFMAs apart).
-        constexpr int LGL = G::GL_BLOCKS - 1;  // the softmax follows this block: its tile is flushed, not deferred
-        constexpr int LB = G::BLOCKS - 1;      // the component's last table block: flushed
-        f64x4 AX[2][CT], AY[2][CT];
-        double qp[CT], p[CT];
-        double bs0[CT], bs1[CT], bs1p[CT];
-#pragma unroll
-        for (int c = 0; c < CT; ++c) {
-          qp[c] = 0.0;
-          p[c] = 0.0;
-          bs0[c] = bs1[c] = bs1p[c] = 0.0;
-#pragma unroll
-          for (int i = 0; i < 2; ++i) AX[i][c] = AY[i][c] = f64x4{0.0, 0.0, 0.0, 0.0};
-        }
-        auto foldt = [&](f64x4 (&x)[CT], f64x4 (&yy)[CT]) {
-#pragma unroll
-          for (int c = 0; c < CT; ++c) {
-            const f64x4 v = x[c] + yy[c];
-            qp[c] = fma(v[0], v[0], qp[c]);
-            qp[c] = fma(v[1], v[1], qp[c]);
-            qp[c] = fma(v[2], v[2], qp[c]);
-            qp[c] = fma(v[3], v[3], qp[c]);
-            asm volatile("" : "+v"(qp[c]));
-            x[c] = f64x4{0.0, 0.0, 0.0, 0.0};
-            yy[c] = x[c];
-          }
-        };
-        constexpr int NB = E + 2;  // operand slots: block b-1's a.y is still needed during step b
-        double2 buf[NB];
-#pragma unroll
-        for (int i = 0; i < E; ++i) buf[i] = rd(i * 1024);
-        static_for(
-            [&](auto bc) {
-              constexpr int b = decltype(bc)::value;
-              constexpr BlockInfo bi = block_info<MP, NP, HM>(b);
-              constexpr BlockInfo pv = block_info<MP, NP, HM>(b > 0 ? b - 1 : G::BPC);
-              constexpr bool DATA = bi.kind == 0 || bi.kind == 2;
-              constexpr bool PDATA = b > 0 && (pv.kind == 0 || pv.kind == 2);
-              constexpr bool PEND = PDATA && (b - 1) != LGL && (b - 1) != LB;  // y-half of b-1 issued here
-              constexpr bool FLUSH = DATA && (b == LGL || b == LB);              // own y-half issued here too
-              __builtin_amdgcn_sched_barrier(0);
-              constexpr bool RB = (b + E) % G::CB == 0;
-              if constexpr (RB) {
-                F64_STAMP(bi.kind <= 1 ? 0 : 2);
-                boundary_wait();
-                refill_begin();
-              }
-              if constexpr (b + E < G::BPC) {
-                constexpr int r = b + E;
-                if constexpr (r % G::CB == 0) {
-                  rslot = rslot + 1 == G::NSLOT ? 0 : rslot + 1;
-                  roff = lane * 16 + rslot * G::CHUNK;
-                  asm volatile("" : "+v"(roff));
-                }
-                buf[r % NB] = rd((r % G::CB) * 1024);
-              }
-              const double2 a = buf[b % NB];
-              const double2 ap = buf[(b + NB - 1) % NB];
-              constexpr int NMF = (bi.kind == 4 ? 0 : CT) + (PEND ? CT : 0) + (FLUSH ? CT : 0);
-              int jm = 0;
-              auto gap = [&]() {
-                if constexpr (RB && NMF > 0) {
-                  __builtin_amdgcn_sched_barrier(0);
-                  refill_pieces(jm * LPW / NMF, (jm + 1) * LPW / NMF);
-                  __builtin_amdgcn_sched_barrier(0);
-                }
-                ++jm;
-              };
-              if constexpr (bi.kind == 2 && bi.T == 0) {  // new GW k-pair: B operands of this k-pair (keep the last)
-#pragma unroll
-                for (int c = 0; c < CT; ++c) {
-                  bs1p[c] = bs1[c];
-                  bs0[c] = yv[c][bi.s].x * p[c];
-                  bs1[c] = yv[c][bi.s].y * p[c];
-                }
-              }
-              // the deferred half of block b-1
-              auto pending = [&]() {
-                if constexpr (PEND) {
-                  if constexpr (pv.kind == 0) {
-#pragma unroll
-                    for (int c = 0; c < CT; ++c) {
-                      AY[pv.T & 1][c] = mfma16x16x4d(ap.y, yv[c][pv.s].y, AY[pv.T & 1][c]);
-                      gap();
-                    }
-                  } else {
-#pragma unroll
-                    for (int c = 0; c < CT; ++c) {
-                      out[pv.T][c] = mfma16x16x4d(ap.y, pv.s == bi.s ? bs1[c] : bs1p[c], out[pv.T][c]);
-                      gap();
-                    }
-                  }
-                }
-              };
-              if constexpr (FLUSH) pending();
-              // this block's first half (or its only MFMA: the mean columns)
-              if constexpr (bi.kind == 0) {
-#pragma unroll
-                for (int c = 0; c < CT; ++c) {
-                  AX[bi.T & 1][c] = mfma16x16x4d(a.x, yv[c][bi.s].x, AX[bi.T & 1][c]);
-                  gap();
-                }
-              } else if constexpr (bi.kind == 1) {
-                const double one = g == 0 ? 1.0 : 0.0;
-#pragma unroll
-                for (int c = 0; c < CT; ++c) {
-                  AX[bi.T & 1][c] = mfma16x16x4d(a.x, one, AX[bi.T & 1][c]);
-                  gap();
-                }
-              } else if constexpr (bi.kind == 2) {
-#pragma unroll
-                for (int c = 0; c < CT; ++c) {
-                  out[bi.T][c] = mfma16x16x4d(a.x, bs0[c], out[bi.T][c]);
-                  gap();
-                }
-              } else if constexpr (bi.kind == 3) {
-#pragma unroll
-                for (int c = 0; c < CT; ++c) {
-                  out[bi.T][c] = mfma16x16x4d(a.x, g == 0 ? p[c] : 0.0, out[bi.T][c]);
-                  gap();
-                }
-              }
-              if constexpr (!FLUSH) pending();
-              if constexpr (FLUSH) {  // own second half now (the softmax / the component end follows)
-                if constexpr (bi.kind == 0) {
-#pragma unroll
-                  for (int c = 0; c < CT; ++c) {
-                    AY[bi.T & 1][c] = mfma16x16x4d(a.y, yv[c][bi.s].y, AY[bi.T & 1][c]);
-                    gap();
-                  }
-                } else {
-#pragma unroll
-                  for (int c = 0; c < CT; ++c) {
-                    out[bi.T][c] = mfma16x16x4d(a.y, bs1[c], out[bi.T][c]);
-                    gap();
-                  }
-                }
-              }
-              if constexpr (RB && NMF == 0) refill_pieces(0, LPW);
-              // fold tile T-1 at tile T's second step, two or more MFMAs after its last half was issued (its mean
-              // step, or the deferred half in tile T's first step); the last tile folds at once, the softmax needs it
-              if constexpr (bi.kind == 0 && bi.T >= 1 && bi.s == 1) foldt(AX[(bi.T - 1) & 1], AY[(bi.T - 1) & 1]);
-              if constexpr (b == LGL) {
-                foldt(AX[bi.T & 1], AY[bi.T & 1]);
-                F64_STAMP(0);
-                double lp[CT];
-                bool need = false;
-#pragma unroll
-                for (int c = 0; c < CT; ++c) {
-                  lp[c] = ck - sum_groups(qp[c]);
-                  need = need || (lp[c] > m[c] + RESCALE);
-                }
-                if (__builtin_amdgcn_ballot_w64(need) != 0ull) {  // rare: new running maximum
-#pragma unroll
-                  for (int c = 0; c < CT; ++c) {
-                    const bool up = lp[c] > m[c] + RESCALE;
-                    const double mn = up ? lp[c] : m[c];
-                    const double al = up ? (m[c] == QCE_NEG_INF ? 0.0 : exp(m[c] - mn)) : 1.0;
-                    ssum[c] *= al;
-                    m[c] = mn;
-#pragma unroll
-                    for (int T = 0; T < G::NTW; ++T) out[T][c] *= al;
-                  }
-                }
-#pragma unroll
-                for (int c = 0; c < CT; ++c) {
-                  p[c] = (lp[c] == QCE_NEG_INF) ? 0.0 : exp(lp[c] - m[c]);
-                  ssum[c] += p[c];
-                }
-                F64_STAMP(1);
-              }
-            },
-            std::make_integer_sequence<int, G::BPC>{});
-      }
       F64_STAMP(2);
       cstream += G::CPC;
     }
@@ -696,46 +512,11 @@ __global__ __launch_bounds__(NW * 64, BUD < 144 ? 2 : 1) void k_est_all_f64(long
 // or a 128-row output accumulator, take the registers of two 64-dim ones)
 constexpr int qce_f64_ct(int MP, int NP) { return (MP <= 64 && NP <= 64) ? 2 : 1; }
 
-// workgroup shape of the launch: 8 (one 8-wave workgroup per CU), 4 (one 4-wave workgroup, two column tiles per
-// wave) or 42 (two 4-wave workgroups per CU) -- 42 only where the two-workgroup ring reads the packed layout
-template <int MP, int NP, bool HM>
-constexpr bool qce_f64_dual_shape() {
-  return qce_f64_ct(MP, NP) == 2 && f64_dual_ok(F64G<MP, NP, HM>::BLOCKS);
-}
-
 template <int MP, int NP, bool HM, bool OP>
 hipError_t qce_f64_launch_t(const QceF64Args& a, hipStream_t st) {
   constexpr int CT0 = qce_f64_ct(MP, NP);
-  if constexpr (CT0 == 1) {
-    if (a.pipe) {  // one wave per SIMD: the deferred-half issue order (QCE_F64_PIPE)
-      hipLaunchKernelGGL((k_est_all_f64<MP, NP, HM, 1, 4, OP, 144, true>), dim3((unsigned)a.nwg), dim3(4 * 64), 0, st,
-                         a.B, a.M, a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa,
-                         a.pk, a.shift, a.stamps);
-      return hipGetLastError();
-    }
-  }
-  if constexpr (CT0 == 2 && f64_dual_ok(F64G<MP, NP, HM>::BLOCKS)) {
-    if (a.waves == 42 && a.pipe) {
-      hipLaunchKernelGGL((k_est_all_f64<MP, NP, HM, 1, 4, OP, 72, true>), dim3((unsigned)a.nwg), dim3(4 * 64), 0, st,
-                         a.B, a.M, a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa,
-                         a.pk, a.shift, a.stamps);
-      return hipGetLastError();
-    }
-    if (a.waves == 42) {  // two 4-wave workgroups per CU, one column tile per wave
-      hipLaunchKernelGGL((k_est_all_f64<MP, NP, HM, 1, 4, OP, 72>), dim3((unsigned)a.nwg), dim3(4 * 64), 0, st, a.B,
-                         a.M, a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa, a.pk,
-                         a.shift, a.stamps);
-      return hipGetLastError();
-    }
-  }
   if constexpr (CT0 == 2) {
-    if ((a.waves == 8 || a.waves == 42) && a.pipe) {
-      hipLaunchKernelGGL((k_est_all_f64<MP, NP, HM, 1, 8, OP, 144, true>), dim3((unsigned)a.nwg), dim3(8 * 64), 0, st,
-                         a.B, a.M, a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa,
-                         a.pk, a.shift, a.stamps);
-      return hipGetLastError();
-    }
-    if (a.waves == 8 || a.waves == 42) {  // two waves per SIMD, one column tile each (same tile of 128 samples)
+    if (a.waves == 8) {  // two waves per SIMD, one column tile each (same tile of 128 samples)
       hipLaunchKernelGGL((k_est_all_f64<MP, NP, HM, 1, 8, OP>), dim3((unsigned)a.nwg), dim3(8 * 64), 0, st, a.B, a.M,
                          a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa, a.pk,
                          a.shift, a.stamps);

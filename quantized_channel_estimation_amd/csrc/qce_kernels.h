@@ -102,13 +102,10 @@ struct QceF64Args {
   double* pk = nullptr;   // shifted packed partial B x (2N+2): [s e^{m-shift}, 0, acc e^{m-shift}] (instead of om/os/oa)
   const double* shift = nullptr;  // device pointer: the shared shift M* of the packed partial
   unsigned long long* stamps = nullptr;  // diagnostic builds (-DQCE_STAMPS): per-wave segment cycles
-  int pipe = 0;   // deferred-half MFMA issue order (QCE_F64_PIPE=1)
-  int waves = 8;  // workgroup shape where M, N <= 64: 8 waves x 1 column tile (two per SIMD), 4 x 2 (QCE_F64_WAVES=4),
-                  // or 42: two 4-wave workgroups per CU (QCE_F64_WAVES=42)
+  int waves = 8;  // workgroup shape where M, N <= 64: 8 waves x 1 column tile (two per SIMD), or 4 x 2 (QCE_F64_WAVES=4)
 };
 bool qce_f64_shape(int MP, int NP);
-int qce_f64_tile(int MP, int NP, int waves);  // samples per workgroup tile of the launch shape `waves` (8 / 4 / 42)
-bool qce_f64_dual(int MP, int NP, int has_mean);  // the two-workgroups-per-CU shape (42) exists for this model
+int qce_f64_tile(int MP, int NP);  // samples per workgroup tile
 long long qce_pack_f64all_bytes(int MP, int NP, int has_mean);
 hipError_t qce_launch_pack_f64all(int K, int M, int N, int MP, int NP, int has_mean, const double2* Linv,
                                   const double2* W, const double2* q0, const double2* bvec, double* pack,

@@ -771,10 +771,7 @@ int qce_kshard_prepare(qce_kshard* ks, const double* A, int M, double snr_db, do
   const int j = dbl ? 1 - ks->cur : 0;
   qce_model* m = ks->mods[j];
   hipStream_t ps = dbl ? ks->ps : st;
-  if (dbl) {
-    KS_HIP(hipStreamWaitEvent(ps, ks->ev_done, 0));  // no-op before the first step; orders any repair of that step
-    if (ks->used_valid[j]) KS_HIP(hipStreamWaitEvent(ps, ks->ev_used[j], 0));
-  }
+  if (dbl && ks->used_valid[j]) KS_HIP(hipStreamWaitEvent(ps, ks->ev_used[j], 0));
   if (ks->pending.valid && ks->pending.model == m) ks->pending.stale = 1;  // its tables are being replaced
   ks->cur = j;
   ks->m = m;
@@ -788,7 +785,9 @@ int qce_kshard_prepare(qce_kshard* ks, const double* A, int M, double snr_db, do
     KS_HIP(hipMemcpyAsync(shift, &inf, sizeof(double), hipMemcpyHostToDevice, ps));
     KS_HIP(hipStreamSynchronize(ps));
   }
-  // the shift MAX is ordered after the previous step's collectives (ev_done above): one communicator, one order
+  // the shift MAX is ordered after the previous step's collectives: one communicator, one order on every rank (the
+  // prepare's kernels above overlap that step; only this 8-byte collective waits for it)
+  if (dbl) KS_HIP(hipStreamWaitEvent(ps, ks->ev_done, 0));  // no-op before the first step
   KS_RC(collective(ks->c, QCE_COLL_ALLREDUCE_MAX, shift, shift, 1, ps));
   if (const char* b = getenv("QCE_KSHARD_SHIFT_BIAS")) {  // tests only: force the underflow path
     hipLaunchKernelGGL(k_ks_add, dim3(1), dim3(64), 0, ps, shift, atof(b));

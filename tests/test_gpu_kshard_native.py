@@ -266,10 +266,14 @@ def test_host_transport_multirank_all_and_selective_modes(world, mname):
                 assert sorted(cover) == list(range(len(set(cover)))), (m, sc)
     for rank, out, rep in res:
         for tag, mtag, chunks, scatter, r, eo, er in out:
-            tol = 1e-6 if tag.startswith("p2_b1") else 1e-9
+            # the documented sensitivities (tests/test_gpu_parity.py): 1 bit with a general A (arcsine
+            # law near |rho| = 1), and 1 bit on the Fourier path (the dense reference's circulant Cy differs in its
+            # last bits along a diagonal) -- 1e-6 / 1e-7; everything else 1e-9
+            tol = 1e-6 if tag.startswith("p2_b1") else (1e-7 if mname in ("circ", "bcirc") and tag.startswith("b1") else 1e-9)
             assert eo < tol, (rank, tag, mtag, chunks, scatter, eo)
             assert er < H_TOL, (rank, tag, mtag, chunks, scatter, er)
-        assert rep < 1e-9, (rank, rep)
+        tol = 1e-7 if mname in ("circ", "bcirc") else 1e-9  # the first case is 1 bit (see above)
+        assert rep < tol, (rank, rep)
 
 
 def _chol_worker(rank, world, port, sync, q):

@@ -20,9 +20,11 @@ run lds "$BARGS" SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INST
 run fetch "" FETCH_SIZE || exit $?
 run write "" WRITE_SIZE || exit $?
 run tcc "" TCC_HIT_sum TCC_MISS_sum || exit $?
+run dram "" TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum || exit $?
 if [ "${CAL:-0}" = "1" ]; then
   run cfetch "--components 1" FETCH_SIZE || exit $?
   run cwrite "--components 1" WRITE_SIZE || exit $?
+  run cdram "--components 1" TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_DRAM_sum || exit $?
 fi
 cd $R
 BID=$(python3 -c "from quantized_channel_estimation_amd import _lib; print(_lib.build_id())")

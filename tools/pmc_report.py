@@ -37,7 +37,7 @@ def load(name):
     return {k: sum(v) / len(v) for k, v in out.items()}, t
 
 
-res = {p: load(p) for p in ("sq", "inst", "lds", "fetch", "write", "tcc", "cfetch", "cwrite")}
+res = {p: load(p) for p in ("sq", "inst", "lds", "fetch", "write", "tcc", "dram", "cfetch", "cwrite", "cdram")}
 print(f"kernel pattern {pat!r}, config {cfg} (B={B}, N={N}), library build {bid}")
 for p, (v, t) in res.items():
     for k, x in sorted(v.items()):
@@ -81,9 +81,26 @@ if f and w:
         cal = dict(read_ratio=2 * cf * 1024 / (16 * N * B), write_ratio=cw * 1024 / (16 * N * B))
         print(f"K=1 calibration: 2*FETCH / y bytes = {cal['read_ratio']:.3f}, WRITE / h bytes = {cal['write_ratio']:.3f}")
     kern = "fft" if pat.startswith("k_fft") else "f64"
+    # DRAM-side requests (TCC_EA0_{RD,WR}REQ_DRAM: L2 misses that went to HBM, not the Infinity Cache); bytes per
+    # request from the K=1 calibration of the kernel's own y / h pattern when present, else 64 B
+    dram = None
+    dr, _ = res["dram"]
+    if dr:
+        rq, wq = dr.get("TCC_EA0_RDREQ_DRAM_sum", 0.0), dr.get("TCC_EA0_WRREQ_DRAM_sum", 0.0)
+        cd, _ = res["cdram"]
+        rb = wb = 64.0
+        basis = "64 B per request (no calibration pass)"
+        if cd and cd.get("TCC_EA0_RDREQ_DRAM_sum") and cd.get("TCC_EA0_WRREQ_DRAM_sum"):
+            rb = 16.0 * N * B / cd["TCC_EA0_RDREQ_DRAM_sum"]
+            wb = 16.0 * N * B / cd["TCC_EA0_WRREQ_DRAM_sum"]
+            basis = f"bytes per request calibrated on the K=1 run (read {rb:.1f} B, write {wb:.1f} B)"
+        dram = dict(bytes_per_launch=rq * rb + wq * wb, read_requests=rq, write_requests=wq, basis=basis)
+        print(f"DRAM (HBM) side: {rq:.4g} read + {wq:.4g} write requests -> {dram['bytes_per_launch'] / 1e6:.1f} MB "
+              f"= {dram['bytes_per_launch'] / alg:.2f}x algorithmic ({basis})")
     json.dump({"config": cfg, "B": B, "kernel": kern, "kernel_name": pat, "build_id": bid,
-               "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": alg,
+               "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": alg, "dram": dram,
                "fetch_size_kb": f, "write_size_kb": w, "calibration_k1": cal,
-               "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, FETCH doubled (gfx950); "
-                       "tools/pmc_kernel.sh + tools/pmc_report.py"},
+               "note": "hbm_bytes_per_launch: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, FETCH "
+                       "doubled (gfx950), as MI355X_MICROARCH.md prescribes -- it counts L2 misses served by the "
+                       "Infinity Cache too; dram: the requests that reached HBM; tools/pmc_kernel.sh + pmc_report.py"},
               open(os.path.join(base, f"traffic_{cfg}.json"), "w"), indent=1)
