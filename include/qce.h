@@ -283,7 +283,7 @@ int qce_kshard_destroy(qce_kshard* ks);
 /* Double-buffered tables: `spare` is a second model of the same shard (same parameters; not owned).  Prepares then
  * alternate between the two table sets on the library's prepare stream: prepare t+1 waits only for the last step
  * that read its set (step t-1), so it runs beside step t's partial kernels (Bussgang_GMM.py:284-287: the next SNR
- * point's tables do not depend on the current estimate); its shift MAX is ordered after step t's collectives. */
+ * point's tables do not depend on the current estimate); its shift MAX runs on a second (control) communicator. */
 int qce_kshard_set_spare(qce_kshard* ks, qce_model* spare);
 /* Per-SNR prepare of the shard (qce_prepare) and the shared shift M* = max over ALL components of
  * c_k = -M log(pi) + 2 log det P_k + log w_k (>= every lp: the quad form is >= 0), one MAX all-reduce on `stream`
@@ -299,8 +299,10 @@ int qce_kshard_prepare(qce_kshard* ks, const double* A, int M, double snr_db, do
  * every rank selects the same components (k_select on the full lp) and the shards' weighted filter sums are
  * summed (one chunk).  h_out: device memory, the rows qce_kshard_rows names.  A 2-double MAX of the step's flag
  * word [rows whose shifted sum underflowed, Cholesky failure on any rank] closes the step; nothing is read on the
- * host until qce_kshard_finish.  y and h_out must stay valid until then.  The caller's `stream` is ordered after
- * the step's collectives. */
+ * host until qce_kshard_finish.  The step's collectives and row finalisation run on the library's communication
+ * stream and may still be in flight when the next step's kernels start on `stream` (the send rows alternate between
+ * two buffers); h_out is complete once qce_kshard_finish returned, which also orders `stream` after the step.  y and
+ * every h_out since the last finish must stay valid until then. */
 int qce_kshard_estimate(qce_kshard* ks, const double* y, int64_t B, int mode, double mode_param, int chunks,
                         int scatter, double* h_out, void* stream);
 /* The caller's sync point: reads the flag words (one host synchronisation).  QCE_ECHOL with the reference's

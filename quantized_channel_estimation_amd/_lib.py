@@ -550,10 +550,14 @@ class KShard:
             raise ValueError(f"y must have {self.model.M} columns, got {y.shape[1]}")
         check(load().qce_kshard_estimate(self._h, ptr(y), int(B), int(mode), float(param), ch, int(bool(scatter)),
                                          ptr(out), stream))
-        self._keep = (y, out)  # y and h must stay alive until finish()
+        # y and every h since the last finish() stay alive until then: the steps' collectives and row finalisation
+        # may still write h on the library's communication stream
+        self._keep = (self._keep or []) + [(y, out)]
         return rows, out
 
     def finish(self, stream=None):
+        """The sync point: flag words read, Cholesky errors raised, flagged rows recombined; `stream` (the caller's)
+        is ordered after the steps' collectives."""
         try:
             check(load().qce_kshard_finish(self._h, stream))
         finally:

@@ -278,7 +278,9 @@ struct KBuf {
 
 struct qce_comm {
   int rank = 0, world = 1, device = 0, kind = QCE_COMM_RCCL;
-  ncclComm_t nc = nullptr;
+  ncclComm_t nc = nullptr;      // data collectives of the steps (issued only from the K-shard's communication stream)
+  ncclComm_t nc_ctl = nullptr;  // the per-SNR shift MAX (issued only from the prepare stream): a second communicator
+                                // (ncclCommSplit), so the next prepare need not wait for the current step's collectives
   qce_host_collective fn = nullptr;
   void* user = nullptr;
   double *pin_send = nullptr, *pin_recv = nullptr;  // host transport staging
@@ -300,7 +302,11 @@ struct qce_kshard {
   hipStream_t cs = nullptr;  // communication stream: the chunks' collectives and row finalisation
   std::vector<hipEvent_t> ev_chunk;
   hipEvent_t ev_done = nullptr;
-  KBuf<double> shift, fl, earlier, pk, rs;  // shift: one slot per table set
+  KBuf<double> shift, fl, earlier, rs;  // shift: one slot per table set
+  KBuf<double> pkb[2];                  // the steps' send rows, alternating: step t+1's kernels fill one while step
+  int pkp = 0;                          // t's collectives still read the other
+  KBuf<double> step_shift;              // [parity]: the shift a step used (its flag word reads it on the comm stream)
+  hipEvent_t ev_st2cs = nullptr, ev_cs2st = nullptr;
   KBuf<unsigned> cnt;
   double* host_fl = nullptr;  // pinned: [fl0, fl1, earlier0, earlier1] of the last step
   int local_chol = 0;         // this rank's library refused a call with the reference's Cholesky error
@@ -330,17 +336,19 @@ int comm_error(const std::string& what, ncclResult_t r) {
 }
 
 // one collective of doubles on stream st (see the QCE_COLL_* semantics in qce.h)
-int collective(qce_comm* c, int op, const double* send, double* recv, long long count, hipStream_t st) {
+int collective(qce_comm* c, int op, const double* send, double* recv, long long count, hipStream_t st,
+               bool ctl = false) {
   if (count <= 0) return QCE_OK;
   if (c->kind == QCE_COMM_RCCL) {
     ncclResult_t r;
+    ncclComm_t nc = ctl ? c->nc_ctl : c->nc;
     switch (op) {
-      case QCE_COLL_ALLREDUCE_SUM: r = ncclAllReduce(send, recv, (size_t)count, ncclFloat64, ncclSum, c->nc, st); break;
-      case QCE_COLL_ALLREDUCE_MAX: r = ncclAllReduce(send, recv, (size_t)count, ncclFloat64, ncclMax, c->nc, st); break;
+      case QCE_COLL_ALLREDUCE_SUM: r = ncclAllReduce(send, recv, (size_t)count, ncclFloat64, ncclSum, nc, st); break;
+      case QCE_COLL_ALLREDUCE_MAX: r = ncclAllReduce(send, recv, (size_t)count, ncclFloat64, ncclMax, nc, st); break;
       case QCE_COLL_REDUCE_SCATTER_SUM:
-        r = ncclReduceScatter(send, recv, (size_t)count, ncclFloat64, ncclSum, c->nc, st);
+        r = ncclReduceScatter(send, recv, (size_t)count, ncclFloat64, ncclSum, nc, st);
         break;
-      case QCE_COLL_ALLGATHER: r = ncclAllGather(send, recv, (size_t)count, ncclFloat64, c->nc, st); break;
+      case QCE_COLL_ALLGATHER: r = ncclAllGather(send, recv, (size_t)count, ncclFloat64, nc, st); break;
       default: return qce_set_error(QCE_EARG, "unknown collective");
     }
     if (r != ncclSuccess) return comm_error("RCCL collective", r);
@@ -417,7 +425,7 @@ int reduce_chunks(qce_kshard* ks, const std::vector<Chunk>& L, bool scatter, int
   hipEvent_t ev = ks->ev_chunk[chunk_index];
   KS_HIP(hipEventRecord(ev, st));
   KS_HIP(hipStreamWaitEvent(ks->cs, ev, 0));
-  double* send = ks->pk.p + ch.pk_off * W;
+  double* send = ks->pkb[ks->pkp].p + ch.pk_off * W;
   const double* rows;
   if (scatter) {
     const long long q = ch.npad / c->world;
@@ -446,15 +454,28 @@ int ensure_events(qce_kshard* ks, size_t n) {
 }
 
 // close a step: flag word MAX, pinned copy of [fl, earlier], the caller's stream ordered behind the comm stream
-int close_step(qce_kshard* ks, hipStream_t st) {
-  hipLaunchKernelGGL(k_ks_flags, dim3(1), dim3(64), 0, ks->cs, ks->cnt.p, ks->shift.p + ks->cur, ks->local_chol,
+int close_step(qce_kshard* ks) {
+  hipLaunchKernelGGL(k_ks_flags, dim3(1), dim3(64), 0, ks->cs, ks->cnt.p, ks->step_shift.p + ks->pkp, ks->local_chol,
                      ks->fl.p);
   KS_HIP(hipGetLastError());
   KS_RC(collective(ks->c, QCE_COLL_ALLREDUCE_MAX, ks->fl.p, ks->fl.p, 2, ks->cs));
   KS_HIP(hipMemcpyAsync(ks->host_fl, ks->fl.p, 2 * sizeof(double), hipMemcpyDeviceToHost, ks->cs));
   KS_HIP(hipMemcpyAsync(ks->host_fl + 2, ks->earlier.p, 2 * sizeof(double), hipMemcpyDeviceToHost, ks->cs));
-  KS_HIP(hipEventRecord(ks->ev_done, ks->cs));
-  KS_HIP(hipStreamWaitEvent(st, ks->ev_done, 0));
+  KS_HIP(hipEventRecord(ks->ev_done, ks->cs));  // h_out complete (the caller's stream waits for it in finish)
+  return QCE_OK;
+}
+
+// stream hand-offs: every data collective is issued on the communication stream (one stream per communicator)
+int st_to_cs(qce_kshard* ks, hipStream_t st) {
+  if (st == ks->cs) return QCE_OK;
+  KS_HIP(hipEventRecord(ks->ev_st2cs, st));
+  KS_HIP(hipStreamWaitEvent(ks->cs, ks->ev_st2cs, 0));
+  return QCE_OK;
+}
+int cs_to_st(qce_kshard* ks, hipStream_t st) {
+  if (st == ks->cs) return QCE_OK;
+  KS_HIP(hipEventRecord(ks->ev_cs2st, ks->cs));
+  KS_HIP(hipStreamWaitEvent(st, ks->ev_cs2st, 0));
   return QCE_OK;
 }
 
@@ -470,7 +491,8 @@ int step_all(qce_kshard* ks, qce_model* m, const double2* y, long long B, int ch
     pk_rows += ch.npad;
     if (scatter) rs_rows += ch.npad / c->world;
   }
-  KS_HIP(ks->pk.ensure((size_t)pk_rows * W));
+  KBuf<double>& pkbuf = ks->pkb[ks->pkp];
+  KS_HIP(pkbuf.ensure((size_t)pk_rows * W));
   if (scatter) KS_HIP(ks->rs.ensure((size_t)rs_rows * W));
   KS_RC(ensure_events(ks, L.size()));
   int hard = QCE_OK;
@@ -486,12 +508,14 @@ int step_all(qce_kshard* ks, qce_model* m, const double2* y, long long B, int ch
       KS_HIP(hipMemsetAsync(ks->rm.p, 0xff, sizeof(double) * B, st));  // NaN rows; the Cholesky flag raises first
     }
     KS_HIP(hipMemcpyAsync(ks->mg.p, ks->rm.p, sizeof(double) * B, hipMemcpyDeviceToDevice, st));
-    KS_RC(collective(c, QCE_COLL_ALLREDUCE_MAX, ks->mg.p, ks->mg.p, B, st));
+    KS_RC(st_to_cs(ks, st));
+    KS_RC(collective(c, QCE_COLL_ALLREDUCE_MAX, ks->mg.p, ks->mg.p, B, ks->cs));
+    KS_RC(cs_to_st(ks, st));
   }
   for (size_t i = 0; i < L.size(); ++i) {
     const Chunk& ch = L[i];
     const long long n = ch.hi - ch.lo;
-    double* pk = ks->pk.p + ch.pk_off * W;
+    double* pk = pkbuf.p + ch.pk_off * W;
     if (ch.npad > n) KS_HIP(hipMemsetAsync(pk + n * W, 0, sizeof(double) * (ch.npad - n) * W, st));
     if (rowshift) {
       hipLaunchKernelGGL(k_ks_pack_rowshift, dim3(grid_for(n * W)), dim3(256), 0, st, n, N, ks->rm.p + ch.lo,
@@ -538,7 +562,8 @@ int step_select(qce_kshard* ks, const double2* y, long long B, int mode, double 
   const long long npad = L[0].npad;
   KS_HIP(ks->lp.ensure((size_t)B * Kl));
   KS_HIP(ks->wloc.ensure((size_t)B * Kl));
-  KS_HIP(ks->pk.ensure((size_t)npad * W));
+  KBuf<double>& pkbuf = ks->pkb[ks->pkp];
+  KS_HIP(pkbuf.ensure((size_t)npad * W));
   if (scatter) KS_HIP(ks->rs.ensure((size_t)(npad / c->world) * W));
   int hard = QCE_OK;
   bool ok = false;
@@ -556,7 +581,9 @@ int step_select(qce_kshard* ks, const double2* y, long long B, int mode, double 
     KS_HIP(ks->gath.ensure((size_t)B * 2 * c->world));
     hipLaunchKernelGGL(k_ks_row_argmax, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, Kl, ks->lp.p, ks->lpad.p);
     KS_HIP(hipGetLastError());
-    KS_RC(collective(c, QCE_COLL_ALLGATHER, ks->lpad.p, ks->gath.p, B * 2, st));
+    KS_RC(st_to_cs(ks, st));
+    KS_RC(collective(c, QCE_COLL_ALLGATHER, ks->lpad.p, ks->gath.p, B * 2, ks->cs));
+    KS_RC(cs_to_st(ks, st));
     hipLaunchKernelGGL(k_ks_argmax_weights, dim3(grid_for(B)), dim3(256), 0, st, B, c->world, c->rank, Kl,
                        ks->gath.p, ks->wloc.p);
     KS_HIP(hipGetLastError());
@@ -568,7 +595,9 @@ int step_select(qce_kshard* ks, const double2* y, long long B, int mode, double 
     KS_HIP(ks->wfull.ensure((size_t)B * K));
     hipLaunchKernelGGL(k_ks_pad, dim3(grid_for(B * Kmax)), dim3(256), 0, st, B, Kl, Kmax, ks->lp.p, ks->lpad.p);
     KS_HIP(hipGetLastError());
-    KS_RC(collective(c, QCE_COLL_ALLGATHER, ks->lpad.p, ks->gath.p, B * Kmax, st));
+    KS_RC(st_to_cs(ks, st));
+    KS_RC(collective(c, QCE_COLL_ALLGATHER, ks->lpad.p, ks->gath.p, B * Kmax, ks->cs));
+    KS_RC(cs_to_st(ks, st));
     hipLaunchKernelGGL(k_ks_assemble, dim3(grid_for(B * K)), dim3(256), 0, st, B, c->world, K, Kmax, ks->gath.p,
                        ks->lpfull.p);
     KS_HIP(hipGetLastError());
@@ -580,24 +609,24 @@ int step_select(qce_kshard* ks, const double2* y, long long B, int mode, double 
   }
   // this shard's share of sum_k w_bk (W_k y_b + b_k), written straight into the collective's rows (a row of 2N
   // doubles is one c128 row of h)
-  if (npad > B) KS_HIP(hipMemsetAsync(ks->pk.p + B * W, 0, sizeof(double) * (npad - B) * W, st));
+  if (npad > B) KS_HIP(hipMemsetAsync(pkbuf.p + B * W, 0, sizeof(double) * (npad - B) * W, st));
   ok = false;
   if (!ks->local_chol) {
-    ok = guarded(ks, qce_weighted_estimate(m, y, B, ks->wloc.p, reinterpret_cast<double2*>(ks->pk.p), st), &hard);
+    ok = guarded(ks, qce_weighted_estimate(m, y, B, ks->wloc.p, reinterpret_cast<double2*>(pkbuf.p), st), &hard);
     if (hard) return hard;
   }
-  if (!ok) KS_HIP(hipMemsetAsync(ks->pk.p, 0, sizeof(double) * B * W, st));
+  if (!ok) KS_HIP(hipMemsetAsync(pkbuf.p, 0, sizeof(double) * B * W, st));
   // SUM over shards on the communication stream, rows straight into h_out
   const Chunk& ch = L[0];
   KS_HIP(hipEventRecord(ks->ev_chunk[0], st));
   KS_HIP(hipStreamWaitEvent(ks->cs, ks->ev_chunk[0], 0));
   if (scatter) {
     const long long q = npad / c->world;
-    KS_RC(collective(c, QCE_COLL_REDUCE_SCATTER_SUM, ks->pk.p, ks->rs.p, q * W, ks->cs));
+    KS_RC(collective(c, QCE_COLL_REDUCE_SCATTER_SUM, pkbuf.p, ks->rs.p, q * W, ks->cs));
     if (ch.nv > 0)
       KS_HIP(hipMemcpyAsync(h, ks->rs.p, sizeof(double) * ch.nv * W, hipMemcpyDeviceToDevice, ks->cs));
   } else {
-    KS_RC(collective(c, QCE_COLL_ALLREDUCE_SUM, ks->pk.p, reinterpret_cast<double*>(h), B * W, ks->cs));
+    KS_RC(collective(c, QCE_COLL_ALLREDUCE_SUM, pkbuf.p, reinterpret_cast<double*>(h), B * W, ks->cs));
   }
   return QCE_OK;
 }
@@ -635,6 +664,12 @@ int qce_comm_init(const void* unique_id, int rank, int world, int device, qce_co
     delete c;
     return comm_error("ncclCommInitRank", r);
   }
+  r = ncclCommSplit(c->nc, 0, rank, &c->nc_ctl, nullptr);
+  if (r != ncclSuccess) {
+    (void)ncclCommDestroy(c->nc);
+    delete c;
+    return comm_error("ncclCommSplit", r);
+  }
   *out = c;
   return QCE_OK;
 }
@@ -657,6 +692,7 @@ int qce_comm_init_host(int rank, int world, int device, qce_host_collective fn, 
 int qce_comm_destroy(qce_comm* c) {
   if (!c) return QCE_OK;
   DevGuard g(c->device);
+  if (c->nc_ctl) (void)ncclCommDestroy(c->nc_ctl);
   if (c->nc) (void)ncclCommDestroy(c->nc);
   if (c->pin_send) (void)hipHostFree(c->pin_send);
   if (c->pin_recv) (void)hipHostFree(c->pin_recv);
@@ -718,6 +754,9 @@ int qce_kshard_create(qce_model* shard, qce_comm* comm, int K_total, qce_kshard*
   hipError_t e = hipStreamCreateWithFlags(&ks->cs, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ks->ev_done, hipEventDisableTiming);
   if (e == hipSuccess) e = ks->shift.ensure(2);
+  if (e == hipSuccess) e = ks->step_shift.ensure(2);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ks->ev_st2cs, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ks->ev_cs2st, hipEventDisableTiming);
   if (e == hipSuccess) e = ks->fl.ensure(2);
   if (e == hipSuccess) e = ks->earlier.ensure(2);
   if (e == hipSuccess) e = ks->cnt.ensure(1);
@@ -736,7 +775,7 @@ int qce_kshard_destroy(qce_kshard* ks) {
   if (!ks) return QCE_OK;
   DevGuard g(ks->device);
   if (ks->cs) (void)hipStreamSynchronize(ks->cs);
-  for (auto* b : {&ks->shift, &ks->fl, &ks->earlier, &ks->pk, &ks->rs, &ks->rm, &ks->rsum, &ks->racc, &ks->mg, &ks->lp,
+  for (auto* b : {&ks->shift, &ks->fl, &ks->earlier, &ks->pkb[0], &ks->pkb[1], &ks->step_shift, &ks->rs, &ks->rm, &ks->rsum, &ks->racc, &ks->mg, &ks->lp,
                   &ks->lpad, &ks->gath, &ks->lpfull, &ks->wfull, &ks->wloc})
     b->release();
   ks->cnt.release();
@@ -746,6 +785,8 @@ int qce_kshard_destroy(qce_kshard* ks) {
     (void)hipEventDestroy(pr.second);
   }
   if (ks->ev_done) (void)hipEventDestroy(ks->ev_done);
+  if (ks->ev_st2cs) (void)hipEventDestroy(ks->ev_st2cs);
+  if (ks->ev_cs2st) (void)hipEventDestroy(ks->ev_cs2st);
   for (int i = 0; i < 2; ++i) {
     if (ks->ev_prep[i]) (void)hipEventDestroy(ks->ev_prep[i]);
     if (ks->ev_used[i]) (void)hipEventDestroy(ks->ev_used[i]);
@@ -785,10 +826,9 @@ int qce_kshard_prepare(qce_kshard* ks, const double* A, int M, double snr_db, do
     KS_HIP(hipMemcpyAsync(shift, &inf, sizeof(double), hipMemcpyHostToDevice, ps));
     KS_HIP(hipStreamSynchronize(ps));
   }
-  // the shift MAX is ordered after the previous step's collectives: one communicator, one order on every rank (the
-  // prepare's kernels above overlap that step; only this 8-byte collective waits for it)
-  if (dbl) KS_HIP(hipStreamWaitEvent(ps, ks->ev_done, 0));  // no-op before the first step
-  KS_RC(collective(ks->c, QCE_COLL_ALLREDUCE_MAX, shift, shift, 1, ps));
+  // the shift MAX runs on the control communicator, issued only from this stream in prepare order on every rank, so
+  // it need not wait for the previous step's data collectives (their own communicator, their own stream)
+  KS_RC(collective(ks->c, QCE_COLL_ALLREDUCE_MAX, shift, shift, 1, ps, true));
   if (const char* b = getenv("QCE_KSHARD_SHIFT_BIAS")) {  // tests only: force the underflow path
     hipLaunchKernelGGL(k_ks_add, dim3(1), dim3(64), 0, ps, shift, atof(b));
     KS_HIP(hipGetLastError());
@@ -830,6 +870,11 @@ int qce_kshard_estimate(qce_kshard* ks, const double* y, int64_t B, int mode, do
   double2* hd = reinterpret_cast<double2*>(h_out);
   const bool dbl = ks->mods[1] != nullptr;
   if (dbl) KS_HIP(hipStreamWaitEvent(st, ks->ev_prep[ks->cur], 0));
+  // this step's send rows: the buffer the previous step's collectives do not read; the shift it uses, kept for
+  // its flag word (the next prepare may overwrite the slot before the comm stream gets there)
+  ks->pkp ^= 1;
+  KS_HIP(hipMemcpyAsync(ks->step_shift.p + ks->pkp, ks->shift.p + ks->cur, sizeof(double), hipMemcpyDeviceToDevice,
+                        st));
   if (B > 0) {
     if (mode == QCE_MODE_ALL) {
       KS_RC(step_all(ks, ks->m, yd, B, chunks, scatter != 0, hd, st, false));
@@ -841,7 +886,8 @@ int qce_kshard_estimate(qce_kshard* ks, const double* y, int64_t B, int mode, do
     KS_HIP(hipEventRecord(ks->ev_used[ks->cur], st));
     ks->used_valid[ks->cur] = 1;
   }
-  KS_RC(close_step(ks, st));
+  KS_RC(st_to_cs(ks, st));  // the flag word reads this step's shift copy
+  KS_RC(close_step(ks));
   ks->pending.valid = 1;
   ks->pending.y = yd;
   ks->pending.B = B;
@@ -873,15 +919,13 @@ int qce_kshard_finish(qce_kshard* ks, void* stream) {
     return qce_set_error(QCE_ESTATE, "the last K-shard estimate had rows whose shifted sum underflowed and "
                                      "qce_kshard_prepare ran before qce_kshard_finish: they cannot be recombined");
   if (f0 > 0.0 && pend.mode == QCE_MODE_ALL) {
-    // exact recombination of the last step (every rank agrees through the MAX of the flag word); ordered after
-    // any prepare already issued on the prepare stream (its MAX collective): one communicator, one order
-    KS_HIP(hipStreamWaitEvent(st, ks->ev_done, 0));
-    if (ks->mods[1]) KS_HIP(hipStreamWaitEvent(st, ks->ev_prep[ks->cur], 0));
-    KS_RC(step_all(ks, pend.model, pend.y, pend.B, pend.chunks, pend.scatter != 0, pend.h, st, true));
+    // exact recombination of the last step (every rank agrees through the MAX of the flag word), all of it on the
+    // communication stream (its collectives are data-communicator work)
+    KS_RC(step_all(ks, pend.model, pend.y, pend.B, pend.chunks, pend.scatter != 0, pend.h, ks->cs, true));
     KS_HIP(hipEventRecord(ks->ev_done, ks->cs));
-    KS_HIP(hipStreamWaitEvent(st, ks->ev_done, 0));
-    KS_HIP(hipStreamSynchronize(st));
+    KS_HIP(hipEventSynchronize(ks->ev_done));
   }
+  KS_HIP(hipStreamWaitEvent(st, ks->ev_done, 0));  // the caller's stream sees h complete
   return QCE_OK;
 }
 

@@ -305,7 +305,9 @@ class ComponentShardEstimator:
                 return None
             idx, h = self._native_rows
             self._native_rows = None
-            self.native.finish()
+            import torch
+            dev = torch.device("cuda", self.dev.device)
+            self.native.finish(stream=torch.cuda.current_stream(dev).cuda_stream)
             return idx, h
         if self._pending is None:
             return None
