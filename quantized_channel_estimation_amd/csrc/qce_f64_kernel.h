@@ -43,10 +43,11 @@ namespace {
 constexpr __host__ __device__ int f64_blocks(int MP, int NP, int hmi) {
   return (MP / 8) * (MP / 8 + 1) + hmi * (MP / 8) + (NP / 8) * (MP / 4 + hmi);
 }
-// minlead: blocks of prefetch lead the ring must keep ((NSLOT - 2) chunks are in flight while one is read).  The
-// shapes with a padded dimension of 128 run one wave per SIMD (their registers), where no second wave covers a ring
-// wait: they keep >= 96 blocks (~12k MFMA cycles) in flight; the 2-waves-per-SIMD shapes take the cheapest layout.
-constexpr __host__ __device__ int f64_minlead(int MP, int NP) { return (MP >= 128 || NP >= 128) ? 96 : 0; }
+// minlead: blocks of prefetch lead the ring must keep ((NSLOT - 2) chunks are in flight while one is read).  Tried in
+// round 4 for the one-wave-per-SIMD shapes (padded 128): >= 96 blocks (CB 24, 6 slots) made cfg4 slower (frac 0.676
+// vs 0.714, profiles/r04_cfg4_deeper_ring.txt: the doubled barrier count costs more than the longer lead saves), so
+// every shape keeps the cheapest layout (minlead 0).
+constexpr __host__ __device__ int f64_minlead(int, int) { return 0; }
 constexpr __host__ __device__ int f64_nslot(int cb) { return 144 / cb < 8 ? 144 / cb : 8; }
 constexpr __host__ __device__ int f64_cb(int n, int minlead = 0) {
   int best = 16;
