@@ -35,6 +35,14 @@
 
 #include <utility>
 
+// LDS operand prefetch distance of the block loop (blocks ahead; the compiler keeps E - 1 reads in flight past each
+// wait).  Metric config, one box (profiles/r04_f64_prefetch_ab.txt): E = 2 frac 0.843, 3 0.847, 4 0.850, 5 0.852,
+// 6 0.854-0.859, 8 0.851, 10 0.844, 12 0.850; cfg4 (one wave per SIMD) unchanged by 2-4.  A/B builds:
+// python -m quantized_channel_estimation_amd.build --variant eN --define QCE_F64_E=N (QCE_LIB selects the library).
+#ifndef QCE_F64_E
+#define QCE_F64_E 6
+#endif
+
 namespace {
 
 // Ring geometry: chunks of CB blocks (1 KB each), NSLOT chunks of LDS.  One barrier per chunk, so CB is as large
@@ -185,7 +193,7 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
   using G = F64G<MP, NP, HM>;
   constexpr int TS = NW * 16 * CT;           // samples per tile
   constexpr int LPW = G::CB / NW;  // global_load_lds per wave per chunk
-  constexpr int E = 2;                        // boundary lead (blocks) = LDS prefetch distance
+  constexpr int E = QCE_F64_E;                // boundary lead (blocks) = LDS prefetch distance
   constexpr double RESCALE = 32.0;            // lazy max: rescale only when lp exceeds m by this
   static_assert(G::CB % NW == 0, "chunk split");
   __shared__ __attribute__((aligned(16))) char lds[G::NSLOT * G::CHUNK];
