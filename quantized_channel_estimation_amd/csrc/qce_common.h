@@ -48,4 +48,19 @@ QCE_DEV f32x16 mfma32x32x2(float a, float b, f32x16 c) { return __builtin_amdgcn
 QCE_DEV f32x4 mfma16x16x4(float a, float b, f32x4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 QCE_DEV f64x4 mfma16x16x4d(double a, double b, f64x4 c) { return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0); }
 
+// 16 B per lane global -> LDS DMA (lane l writes LDS byte dst + 16 l; dst wave-uniform), issued as inline asm.
+// With __builtin_amdgcn_global_load_lds the compiler cannot tell the DMA's LDS bytes from a later ds_read of another
+// ring slot and inserts s_waitcnt vmcnt(0) before the next LDS read after every refill: the wave then waits out the
+// refill's whole L2 / HBM latency once per ring chunk (27 % of MFMA time at one wave per SIMD, cfg4).  The ring
+// code orders LDS itself (explicit vmcnt + s_barrier before a slot is read), and the compiler's own vmcnt counts
+// stay safe: loads it does not know about only make its waits stricter.  M0 is set right before the DMA (the
+// compiler sets M0 itself before every instruction of its own that reads it).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+QCE_DEV void lds_dma16(const void* src, const void* lds_dst) {
+  const unsigned dst = (unsigned)(unsigned long)(__attribute__((address_space(3))) const void*)lds_dst;
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(dst) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 #include "../../include/qce.h"

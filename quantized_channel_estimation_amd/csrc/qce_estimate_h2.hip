@@ -42,8 +42,7 @@ QCE_DEV void stage(const char* __restrict__ src, char* dst, int wave, int lane) 
   wave = __builtin_amdgcn_readfirstlane(wave);  // wave-uniform: no waterfall around the M0 base
 #pragma unroll
   for (int c = wave; c < BYTES / 1024; c += 8) {
-    __builtin_amdgcn_global_load_lds((const void*)(src + c * 1024 + lane * 16),
-                                     (__attribute__((address_space(3))) void*)(dst + c * 1024), 16, 0, 0);
+    lds_dma16(src + c * 1024 + lane * 16, dst + c * 1024);
   }
 }
 
@@ -503,8 +502,7 @@ QCE_DEV void stage4(const char* __restrict__ src, char* dst, int wave, int lane)
   wave = __builtin_amdgcn_readfirstlane(wave);
 #pragma unroll
   for (int c = wave; c < BYTES / 1024; c += 4) {
-    __builtin_amdgcn_global_load_lds((const void*)(src + c * 1024 + lane * 16),
-                                     (__attribute__((address_space(3))) void*)(dst + c * 1024), 16, 0, 0);
+    lds_dma16(src + c * 1024 + lane * 16, dst + c * 1024);
   }
 }
 

@@ -229,10 +229,7 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
     ++issued;
   };
   auto refill_pieces = [&](int lo, int hi) {
-    for (int i = lo; i < hi; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(rsrc + i * NW * 1024),
-                                       (__attribute__((address_space(3))) void*)(lds + rdst + i * NW * 1024), 16, 0,
-                                       0);
+    for (int i = lo; i < hi; ++i) lds_dma16(rsrc + i * NW * 1024, lds + rdst + i * NW * 1024);
   };
   // boundary for stream chunk jn: its loads landed everywhere, and every wave is done with chunk jn - 2,
   // whose slot is refilled (refill_begin + pieces) with chunk jn + NSLOT - 2

@@ -56,8 +56,7 @@ QCE_DEV void x_stage(const char* __restrict__ src, char* dst, int wave, int lane
 #pragma unroll
   for (int i = 0; i < X_OPS; ++i) {
     const int c = wave + X_NW * i;
-    __builtin_amdgcn_global_load_lds((const void*)(src + c * 1024 + lane * 16),
-                                     (__attribute__((address_space(3))) void*)(dst + c * 1024), 16, 0, 0);
+    lds_dma16(src + c * 1024 + lane * 16, dst + c * 1024);
   }
 }
 

@@ -149,8 +149,7 @@ __global__ __launch_bounds__(256, 1) void k_wsum_f64(long long B, int M, int N, 
                       wave * 1024 + lane * 16;
 #pragma unroll
     for (int i = 0; i < G::LPW; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(src + i * NW * 1024),
-                                       (__attribute__((address_space(3))) void*)(dst + i * NW * 1024), 16, 0, 0);
+      lds_dma16(src + i * NW * 1024, dst + i * NW * 1024);
   };
 #pragma unroll 1
   for (int j = 0; j < G::NSLOT - 1; ++j) issue(j);
