@@ -36,11 +36,12 @@
 #include <utility>
 
 // LDS operand prefetch distance of the block loop (blocks ahead; the compiler keeps E - 1 reads in flight past each
-// wait).  Metric config, one box (profiles/r04_f64_prefetch_ab.txt): E = 2 frac 0.843, 3 0.847, 4 0.850, 5 0.852,
-// 6 0.854-0.859, 8 0.851, 10 0.844, 12 0.850; cfg4 (one wave per SIMD) unchanged by 2-4.  A/B builds:
+// wait).  Metric config, one box (profiles/r04_f64_prefetch_ab.txt, builtin DMA): E = 2 frac 0.843, 3 0.847, 4 0.850,
+// 5 0.852, 6 0.854-0.859, 8 0.851, 10 0.844, 12 0.850.  With the inline-asm DMA (profiles/r04_f64_prefetch_ab2.txt):
+// E = 4 / 6 / 8: metric 0.883-0.884 / 0.885 / 0.886-0.889, cfg4 0.842 / 0.843 / 0.847.  A/B builds:
 // python -m quantized_channel_estimation_amd.build --variant eN --define QCE_F64_E=N (QCE_LIB selects the library).
 #ifndef QCE_F64_E
-#define QCE_F64_E 6
+#define QCE_F64_E 8
 #endif
 
 namespace {
