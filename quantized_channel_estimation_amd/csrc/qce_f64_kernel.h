@@ -43,6 +43,10 @@
 #ifndef QCE_F64_E
 #define QCE_F64_E 8
 #endif
+// 1: drain the LDS prefetches before every ring barrier (the round-3 form, kept for A/B builds)
+#ifndef QCE_F64_BND_DRAIN
+#define QCE_F64_BND_DRAIN 0
+#endif
 
 namespace {
 
@@ -140,11 +144,26 @@ QCE_DEV void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N_) : "memory");
 }
 
-QCE_DEV double sum_groups(double q) {  // sum over the four 16-lane groups (all lanes get the total)
-  q += __shfl_xor(q, 16);
-  q += __shfl_xor(q, 32);
-  return q;
+// Sum over the four 16-lane groups (all lanes get the total), (g0 + g1) + (g2 + g3) in every lane.  gfx950's
+// v_permlane16/32_swap exchange rows in the VALU: the softmax's critical path (last GL MFMA -> lp -> exp -> first GW
+// MFMA) no longer waits on two ds_bpermute round trips through the LDS.
+QCE_DEV double swap_sum(double q, bool r32) {
+  const int lo = __double2loint(q), hi = __double2hiint(q);
+  double a, b;
+  if (r32) {
+    const auto pl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto ph = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a = __hiloint2double(ph[0], pl[0]);
+    b = __hiloint2double(ph[1], pl[1]);
+  } else {
+    const auto pl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto ph = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    a = __hiloint2double(ph[0], pl[0]);
+    b = __hiloint2double(ph[1], pl[1]);
+  }
+  return a + b;  // the lower row's value first in both lanes of the pair
 }
+QCE_DEV double sum_groups(double q) { return swap_sum(swap_sum(q, false), true); }
 
 // Source cursor of the ring: which component chunk a workgroup streams next.  Items are the
 // workgroup's (tile, component) work in order: R*K full-round items (components 0..K-1 per tile),
@@ -234,9 +253,14 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
   };
   // boundary for stream chunk jn: its loads landed everywhere, and every wave is done with chunk jn - 2,
   // whose slot is refilled (refill_begin + pieces) with chunk jn + NSLOT - 2
+  // No LDS-read drain before the barrier: the slot refilled after it (chunk jn - 2) was last read by blocks this
+  // wave has already consumed (E < CB), so the E - 1 prefetches in flight (all in chunk jn - 1) may cross it.
+  static_assert(E < G::CB, "the prefetch window must stay inside one chunk");
   auto boundary_wait = [&]() {
     wait_vmcnt<(G::NSLOT - 3) * LPW>();
+#if QCE_F64_BND_DRAIN
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     F64_STAMP(3);
