@@ -118,23 +118,30 @@ __global__ __launch_bounds__(64) void k_pack_f64all(int M, int N, int MP, int NP
                                                     const double2* __restrict__ Linv, const double2* __restrict__ W,
                                                     const double2* __restrict__ q0, const double2* __restrict__ bvec,
                                                     double* __restrict__ pack) {
-  const int b = blockIdx.x, k = blockIdx.y, lane = threadIdx.x;
+  const int pb = blockIdx.x, k = blockIdx.y, lane = threadIdx.x;
   const int NTL = MP / 8, NTW = NP / 8, KP = MP / 4, HMI = has_mean ? 1 : 0;
-  const int gl_blocks = NTL * (NTL + 1) + HMI * NTL;
+  // physical block pb = PR v + h: virtual block v of row half h (f64_pr, qce_f64_kernel.h)
+  const int PR = f64_pr(MP, NP), b = pb / PR, h = pb % PR;
+  const int NTLV = NTL / PR, NTWV = NTW / PR;
+  auto gl_off = [&](int T) { return PR == 1 ? T * (T + 1) + HMI * T : 2 * T * (T - 1) + (4 + HMI) * T; };
+  auto gl_len = [&](int T) { return PR == 1 ? 2 * T + 2 : 4 * T + 4; };
+  const int gl_blocks = gl_off(NTLV);
   int kind = 4, T = 0, s = 0;
   if (b < gl_blocks) {
-    while (b >= (T + 1) * (T + 2) + HMI * (T + 1)) ++T;
-    s = b - (T * (T + 1) + HMI * T);
-    kind = s < 2 * T + 2 ? 0 : 1;
+    while (b >= gl_off(T + 1)) ++T;
+    s = b - gl_off(T);
+    kind = s < gl_len(T) ? 0 : 1;
+    T = PR * T + h;                               // the half's real row tile
+    if (kind == 0 && s >= 2 * T + 2) kind = 4;    // half 0's k-pairs past its diagonal: zero block
   } else {
     const int r = b - gl_blocks;
-    if (r < KP * NTW) {
+    if (r < KP * NTWV) {
       kind = 2;
-      s = r / NTW;
-      T = r % NTW;
-    } else if (r < (KP + HMI) * NTW) {
+      s = r / NTWV;
+      T = PR * (r % NTWV) + h;
+    } else if (r < (KP + HMI) * NTWV) {
       kind = 3;
-      T = r - KP * NTW;
+      T = PR * (r - KP * NTWV) + h;
     }
   }
   const int rho = lane & 15, gk = lane >> 4;
@@ -154,14 +161,14 @@ __global__ __launch_bounds__(64) void k_pack_f64all(int M, int N, int MP, int NP
     const double o = a == 0 ? z.x : z.y;
     v[0] = isL ? -o : o;
   }
-  *reinterpret_cast<double2*>(pack + (((long long)k * bpc + b) * 64 + lane) * 2) = make_double2(v[0], v[1]);
+  *reinterpret_cast<double2*>(pack + (((long long)k * bpc + pb) * 64 + lane) * 2) = make_double2(v[0], v[1]);
 }
 
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 namespace {
-int blocks_per_comp(int MP, int NP, int hm) { return f64_bpc(f64_blocks(MP, NP, hm ? 1 : 0), f64_minlead(MP, NP)); }
+int blocks_per_comp(int MP, int NP, int hm) { return f64_pack_blocks(MP, NP, hm ? 1 : 0); }
 }  // namespace
 
 bool qce_f64_shape(int MP, int NP) {

@@ -62,11 +62,23 @@ constexpr __host__ __device__ int f64_blocks(int MP, int NP, int hmi) {
 // every shape keeps the cheapest layout (minlead 0).
 constexpr __host__ __device__ int f64_minlead(int, int) { return 0; }
 constexpr __host__ __device__ int f64_nslot(int cb) { return 144 / cb < 8 ? 144 / cb : 8; }
-constexpr __host__ __device__ int f64_cb(int n, int minlead = 0) {
-  int best = 16;
+// Row-split wave pairs (PR = 2) for the shapes whose state fills a SIMD with one wave (padded 128 x 128): two waves
+// share 16 samples; wave half h takes the GL row tiles 2j + h -- virtual tile j runs 4j + 4 k-pairs, half 0's last
+// two are zero blocks -- and the GW row tiles 2t + h, so each wave holds half the accumulators and two waves fit a
+// SIMD.  A virtual block is PR physical 1 KB blocks (half h at +h KB); both halves run the same instruction stream.
+constexpr __host__ __device__ int f64_pr(int MP, int NP) { return (MP == 128 && NP == 128) ? 2 : 1; }
+constexpr __host__ __device__ int f64_vblocks(int MP, int NP, int hmi) {
+  if (f64_pr(MP, NP) == 1) return f64_blocks(MP, NP, hmi);
+  const int J = MP / 16;  // virtual GL tiles
+  return 2 * J * (J - 1) + (4 + hmi) * J + (NP / 16) * (MP / 4 + hmi);
+}
+// chunk of cb virtual blocks (cb * pr physical, a multiple of 8 between 16 and 48)
+constexpr __host__ __device__ int f64_cb(int n, int minlead = 0, int pr = 1) {
+  int best = 16 / pr;
   double best_cost = 1e30;
-  for (int cb = 16; cb <= 48; cb += 8) {
-    if ((f64_nslot(cb) - 2) * cb < minlead) continue;
+  for (int cbp = 16; cbp <= 48; cbp += 8) {
+    const int cb = cbp / pr;
+    if ((f64_nslot(cbp) - 2) * cb < minlead) continue;
     const int pad = (n + cb - 1) / cb * cb - n;
     const double cost = (double)pad / n + 2.0 / cb;
     if (cost < best_cost - 1e-12) {
@@ -76,44 +88,56 @@ constexpr __host__ __device__ int f64_cb(int n, int minlead = 0) {
   }
   return best;
 }
-constexpr __host__ __device__ int f64_bpc(int n, int minlead = 0) {
-  return (n + f64_cb(n, minlead) - 1) / f64_cb(n, minlead) * f64_cb(n, minlead);
+constexpr __host__ __device__ int f64_bpc(int n, int minlead = 0, int pr = 1) {
+  return (n + f64_cb(n, minlead, pr) - 1) / f64_cb(n, minlead, pr) * f64_cb(n, minlead, pr);
+}
+// physical 1 KB blocks per component of the pack
+constexpr __host__ __device__ int f64_pack_blocks(int MP, int NP, int hmi) {
+  return f64_bpc(f64_vblocks(MP, NP, hmi), f64_minlead(MP, NP), f64_pr(MP, NP)) * f64_pr(MP, NP);
 }
 
 template <int MP, int NP, bool HM>
 struct F64G {
+  static constexpr int PR = f64_pr(MP, NP);
   static constexpr int NTL = MP / 8;  // GL row tiles (16 real rows = 8 complex rows)
   static constexpr int NTW = NP / 8;  // GW row tiles
+  static constexpr int NTLV = NTL / PR, NTWV = NTW / PR;  // per wave (virtual tiles)
   static constexpr int KP = MP / 4;   // k-pairs (4 complex columns)
   static constexpr int HMI = HM ? 1 : 0;
-  static constexpr int GL_BLOCKS = NTL * (NTL + 1) + HMI * NTL;
-  static constexpr int GW_BLOCKS = NTW * (KP + HMI);
+  // k-pairs of GL (virtual) tile T and its first block
+  static constexpr __host__ __device__ int gl_len(int T) { return PR == 1 ? 2 * T + 2 : 4 * T + 4; }
+  static constexpr __host__ __device__ int gl_off(int T) {
+    return PR == 1 ? T * (T + 1) + HMI * T : 2 * T * (T - 1) + (4 + HMI) * T;
+  }
+  static constexpr int GL_BLOCKS = gl_off(NTLV);
+  static constexpr int GW_BLOCKS = NTWV * (KP + HMI);
   static constexpr int BLOCKS = GL_BLOCKS + GW_BLOCKS;
-  static constexpr int CB = f64_cb(BLOCKS, f64_minlead(MP, NP));  // blocks per ring chunk
-  static constexpr int NSLOT = f64_nslot(CB);
-  static constexpr int CHUNK = CB * 1024;
-  static constexpr int BPC = f64_bpc(BLOCKS, f64_minlead(MP, NP));
+  static constexpr int CB = f64_cb(BLOCKS, f64_minlead(MP, NP), PR);  // virtual blocks per ring chunk
+  static constexpr int CBP = CB * PR;                                  // physical blocks per ring chunk
+  static constexpr int NSLOT = f64_nslot(CBP);
+  static constexpr int CHUNK = CBP * 1024;
+  static constexpr int BPC = f64_bpc(BLOCKS, f64_minlead(MP, NP), PR);
   static constexpr int CPC = BPC / CB;
-  static_assert(BLOCKS == f64_blocks(MP, NP, HMI), "block count");
-  static constexpr __host__ __device__ int gl_off(int T) { return T * (T + 1) + HMI * T; }
+  static_assert(BLOCKS == f64_vblocks(MP, NP, HMI), "block count");
 };
 
-// block b of a component -> kind (0 GL data, 1 GL mean, 2 GW data, 3 GW mean, 4 pad), tile T, k-pair s
 struct BlockInfo {
   int kind, T, s;
 };
+// (virtual) block b of a component -> kind (0 GL data, 1 GL mean, 2 GW data, 3 GW mean, 4 pad), (virtual) tile T,
+// k-pair s
 template <int MP, int NP, bool HM>
-constexpr BlockInfo block_info(int b) {
+constexpr __host__ __device__ BlockInfo block_info(int b) {
   using G = F64G<MP, NP, HM>;
   if (b < G::GL_BLOCKS) {
     int T = 0;
     while (b >= G::gl_off(T + 1)) ++T;
     const int s = b - G::gl_off(T);
-    return BlockInfo{s < 2 * T + 2 ? 0 : 1, T, s};
+    return BlockInfo{s < G::gl_len(T) ? 0 : 1, T, s};
   }
   const int r = b - G::GL_BLOCKS;
-  if (r < G::KP * G::NTW) return BlockInfo{2, r % G::NTW, r / G::NTW};
-  if (r < (G::KP + G::HMI) * G::NTW) return BlockInfo{3, r - G::KP * G::NTW, G::KP};
+  if (r < G::KP * G::NTWV) return BlockInfo{2, r % G::NTWV, r / G::NTWV};
+  if (r < (G::KP + G::HMI) * G::NTWV) return BlockInfo{3, r - G::KP * G::NTWV, G::KP};
   return BlockInfo{4, 0, 0};
 }
 
@@ -211,15 +235,19 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
                                                          double* __restrict__ pk, const double* __restrict__ shift,
                                                          unsigned long long* __restrict__ stamps) {
   using G = F64G<MP, NP, HM>;
-  constexpr int TS = NW * 16 * CT;           // samples per tile
-  constexpr int LPW = G::CB / NW;  // global_load_lds per wave per chunk
-  constexpr int E = QCE_F64_E;                // boundary lead (blocks) = LDS prefetch distance
+  constexpr int PR = G::PR;                   // waves per sample group (row-split pairs: 2)
+  constexpr int TS = NW / PR * 16 * CT;       // samples per tile
+  constexpr int LPW = G::CBP / NW;            // global_load_lds per wave per chunk
+  constexpr int E = PR == 2 ? 4 : QCE_F64_E;  // boundary lead (blocks) = LDS prefetch distance (pairs: registers)
   constexpr double RESCALE = 32.0;            // lazy max: rescale only when lp exceeds m by this
-  static_assert(G::CB % NW == 0, "chunk split");
+  static_assert(G::CBP % NW == 0 && NW % PR == 0, "chunk split");
+  static_assert(PR == 1 || CT == 1, "row-split pairs hold one column tile");
   __shared__ __attribute__((aligned(16))) char lds[G::NSLOT * G::CHUNK];
+  __shared__ double qx[PR == 2 ? NW * 64 : 1];  // pairs: the halves' quad forms
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int hh = wave % PR, sgrp = wave / PR;  // row half, sample group (wave-uniform)
   const int g = lane >> 4, col = lane & 15;
   const long long P = gridDim.x, w = blockIdx.x;
   const long long tiles = (B + TS - 1) / TS;
@@ -288,7 +316,7 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
       klo = (int)((item0 > tK ? item0 : tK) - tK);
       khi = (int)((tK + K < item1 ? tK + K : item1) - tK);
     }
-    const long long sbase = t * TS + (long long)wave * 16 * CT;
+    const long long sbase = t * TS + (long long)sgrp * 16 * CT;
     // y fragments: k-pair s, lane group g -> complex column 4s + g (re: k-step 2s, im: 2s+1).  Rows past B
     // and columns past M are clamped (finite values of the same tensor) instead of masked: a padded column
     // meets zero table entries, an invalid sample is never written.  The laundered lane constants keep the
@@ -309,9 +337,9 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
     }
     wait_vmcnt<0>();
     F64_STAMP(5);
-    f64x4 out[G::NTW][CT];
+    f64x4 out[G::NTWV][CT];
 #pragma unroll
-    for (int T = 0; T < G::NTW; ++T)
+    for (int T = 0; T < G::NTWV; ++T)
 #pragma unroll
       for (int c = 0; c < CT; ++c) out[T][c] = f64x4{0.0, 0.0, 0.0, 0.0};
     double m[CT], ssum[CT];
@@ -329,7 +357,7 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
       // into the next chunk and laundered, so the compiler keeps one live offset instead of hoisting one
       // per chunk of the unrolled component
       int rslot = slot0;
-      int roff = lane * 16 + rslot * G::CHUNK;
+      int roff = lane * 16 + hh * 1024 + rslot * G::CHUNK;
       auto rd = [&](int off) -> double2 { return *reinterpret_cast<const double2*>(&lds[roff + off]); };
       f64x4 acc[CT], accp[CT];
       double qp[CT], p[CT];
@@ -355,7 +383,7 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
       };
       double2 buf[E + 1];
 #pragma unroll
-      for (int i = 0; i < E; ++i) buf[i] = rd(i * 1024);
+      for (int i = 0; i < E; ++i) buf[i] = rd(i * PR * 1024);
       static_for(
           [&](auto bc) {
             constexpr int b = decltype(bc)::value;
@@ -372,10 +400,10 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
               constexpr int r = b + E;
               if constexpr (r % G::CB == 0) {
                 rslot = rslot + 1 == G::NSLOT ? 0 : rslot + 1;
-                roff = lane * 16 + rslot * G::CHUNK;
+                roff = lane * 16 + hh * 1024 + rslot * G::CHUNK;
                 asm volatile("" : "+v"(roff));
               }
-              buf[r % (E + 1)] = rd((r % G::CB) * 1024);
+              buf[r % (E + 1)] = rd((r % G::CB) * PR * 1024);
             }
             const double2 a = buf[b % (E + 1)];
             // MFMAs of this block; on a boundary step the refill pieces are spread over their gaps
@@ -438,10 +466,10 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
             // tile folds at once, the softmax needs it
             if constexpr (bi.kind == 0 || bi.kind == 1) {
               constexpr bool first = bi.kind == 0 && bi.s == 0;
-              if constexpr (first && bi.T > 0) fold(accp);
-              constexpr bool last = HM ? (bi.kind == 1) : (bi.s == 2 * bi.T + 1);
+              if constexpr (first && bi.T > 0 && PR == 1) fold(accp);
+              constexpr bool last = HM ? (bi.kind == 1) : (bi.s == G::gl_len(bi.T) - 1);
               if constexpr (last) {
-                if constexpr (bi.T == G::NTL - 1) {
+                if constexpr (bi.T == G::NTLV - 1 || PR == 2) {  // pairs: the partner wave covers the wait
                   fold(acc);
                 } else {
 #pragma unroll
@@ -456,6 +484,12 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
               F64_STAMP(0);
               double lp[CT];
               bool need = false;
+              if constexpr (PR == 2) {  // the pair's quad forms, (half 0 + half 1) in both waves
+                qx[wave * 64 + lane] = qp[0];
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                const double other = qx[(wave ^ 1) * 64 + lane];
+                qp[0] = hh == 0 ? qp[0] + other : other + qp[0];
+              }
 #pragma unroll
               for (int c = 0; c < CT; ++c) {
                 lp[c] = ck - sum_groups(qp[c]);
@@ -470,7 +504,7 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
                   ssum[c] *= al;
                   m[c] = mn;
 #pragma unroll
-                  for (int T = 0; T < G::NTW; ++T) out[T][c] *= al;
+                  for (int T = 0; T < G::NTWV; ++T) out[T][c] *= al;
                 }
               }
 #pragma unroll
@@ -491,7 +525,7 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
     asm volatile("" : "+v"(gw));
 #pragma unroll
     for (int c = 0; c < CT; ++c) {
-      const int ls = wave * 16 * CT + 16 * c + col;
+      const int ls = sgrp * 16 * CT + 16 * c + col;
       const long long sample = t * TS + ls;
       if (sample >= B) continue;
       const bool whole = (klo == 0 && khi == K);
@@ -500,10 +534,10 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
       if (OUT_PARTIAL && whole && pk) {  // shifted packed partial: [s e^{m-M*}, 0, acc e^{m-M*}] (K-shard sum)
         const double sc = (m[c] == QCE_NEG_INF) ? 0.0 : exp(m[c] - *shift);
         double* dp = pk + sample * (2LL * N + 2);
-        if (g == 0) *reinterpret_cast<double2*>(dp) = make_double2(ssum[c] * sc, 0.0);
+        if (g == 0 && hh == 0) *reinterpret_cast<double2*>(dp) = make_double2(ssum[c] * sc, 0.0);
 #pragma unroll
-        for (int T = 0; T < G::NTW; ++T) {
-          const int i0 = 8 * T + gw, i1 = 8 * T + 4 + gw;
+        for (int T = 0; T < G::NTWV; ++T) {
+          const int i0 = 8 * (PR * T + hh) + gw, i1 = i0 + 4;
           if (i0 < N) *reinterpret_cast<double2*>(dp + 2 + 2 * i0) = make_double2(out[T][c][0] * sc, out[T][c][1] * sc);
           if (i1 < N) *reinterpret_cast<double2*>(dp + 2 + 2 * i1) = make_double2(out[T][c][2] * sc, out[T][c][3] * sc);
         }
@@ -511,13 +545,13 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
         double* dm = whole ? om : pm;
         double* ds = whole ? os : ps;
         double* da = (whole ? oa : pa) + row * (2LL * N);
-        if (g == 0) {
+        if (g == 0 && hh == 0) {
           dm[row] = m[c];
           ds[row] = ssum[c];
         }
 #pragma unroll
-        for (int T = 0; T < G::NTW; ++T) {
-          const int i0 = 8 * T + gw, i1 = 8 * T + 4 + gw;
+        for (int T = 0; T < G::NTWV; ++T) {
+          const int i0 = 8 * (PR * T + hh) + gw, i1 = i0 + 4;
           if (i0 < N) *reinterpret_cast<double2*>(da + 2 * i0) = make_double2(out[T][c][0], out[T][c][1]);
           if (i1 < N) *reinterpret_cast<double2*>(da + 2 * i1) = make_double2(out[T][c][2], out[T][c][3]);
         }
@@ -525,8 +559,8 @@ __global__ __launch_bounds__(NW * 64) void k_est_all_f64(long long B, int M, int
         const double inv = 1.0 / ssum[c];
         double2* hp = h + sample * N;
 #pragma unroll
-        for (int T = 0; T < G::NTW; ++T) {
-          const int i0 = 8 * T + gw, i1 = 8 * T + 4 + gw;
+        for (int T = 0; T < G::NTWV; ++T) {
+          const int i0 = 8 * (PR * T + hh) + gw, i1 = i0 + 4;
           if (i0 < N) hp[i0] = make_double2(out[T][c][0] * inv, out[T][c][1] * inv);
           if (i1 < N) hp[i1] = make_double2(out[T][c][2] * inv, out[T][c][3] * inv);
         }
@@ -554,7 +588,7 @@ hipError_t qce_f64_launch_t(const QceF64Args& a, hipStream_t st) {
       return hipGetLastError();
     }
   }
-  constexpr int CT = CT0, NW = 4;
+  constexpr int CT = CT0, NW = 4 * f64_pr(MP, NP);  // row-split pairs: 8 waves, two per SIMD
   hipLaunchKernelGGL((k_est_all_f64<MP, NP, HM, CT, NW, OP>), dim3((unsigned)a.nwg), dim3(NW * 64), 0, st, a.B, a.M,
                      a.N, a.K, a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa, a.pk, a.shift,
                      a.stamps);
