@@ -288,10 +288,15 @@ def cpu_baseline(cfg, means, covs, w, y, quantizer, budget_s):
 # ------------------------------------------------------------------------------------------ roofline
 def f64_executed_flops(N, K, B):
     """Executed v_mfma_f64_16x16x4 work of k_est_all_f64: 256 flops per sample per 1 KB table block
-    (GL: NTL(NTL+1) blocks — Linv's upper triangle skipped; GW: NTW*KP blocks)."""
+    (GL: NTL(NTL+1) blocks — Linv's upper triangle skipped; GW: NTW*KP blocks).  At padded 128 the row-split wave
+    pairs pad each GL tile pair to 4j + 4 k-pairs per half (qce_f64_kernel.h f64_pr): 4 J (J + 1) GL blocks, J = NTL / 2."""
     Np = 16 if N <= 16 else (32 if N <= 32 else (64 if N <= 64 else 128))
     ntl, ntw, kp = Np // 8, Np // 8, Np // 4
-    return 256.0 * (ntl * (ntl + 1) + ntw * kp) * K * B
+    gl = ntl * (ntl + 1)
+    if Np == 128:  # pairs: virtual tile j (4j + 4 k-pairs) executed by both halves
+        J = ntl // 2
+        gl = 2 * sum(4 * j + 4 for j in range(J))
+    return 256.0 * (gl + ntw * kp) * K * B
 
 
 def dm_has_mean(dm):
