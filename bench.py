@@ -72,6 +72,10 @@ def parse():
                     help="K-shard collectives: native (libqce's own RCCL communicator, qce_kshard_*; torch.distributed "
                          "over gloo only for the rendezvous, barriers and the timing MAX) or a torch.distributed "
                          "backend (nccl = RCCL through torch, gloo) driving sharding.py's Python orchestration")
+    ap.add_argument("--comm", default="auto", choices=["auto", "rccl", "host"],
+                    help="native K-shard communicator: rccl (ncclCommInitRank, one GPU per rank), host (the library's "
+                         "host transport over gloo: ranks may share a GPU) or auto (host when the ranks outnumber the "
+                         "visible GPUs -- the one-GPU rehearsal of the driver's multi-GPU command -- else rccl)")
     ap.add_argument("--collective", default="rs", choices=["rs", "ar"],
                     help="K-shard SUM collective: reduce-scatter (rank keeps its rows) or all-reduce")
     ap.add_argument("--single-buffer", action="store_true",
@@ -441,7 +445,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     # ranks beyond the visible GPUs share them (single-GPU rehearsals of the multi-rank path; on a node
     # with one GPU per rank this is the identity).  device_count() does not initialise the GPU.
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    ndev = torch.cuda.device_count()
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, ndev)
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     if args.batch:
@@ -464,6 +469,7 @@ def main():
             dist.init_process_group("gloo" if native else args.backend)
         world = dist.get_world_size()
     kshard = args.shard == "k" and world > 1
+    comm_kind = None
     qkind = {"uniform": _lib.QUANT_UNIFORM, "lloyd": _lib.QUANT_LLOYD}[cfg["qtype"]]
     thr, lab = (quantizer[0], quantizer[1]) if cfg["n_bits"] not in (1, np.inf) and cfg["qtype"] == "lloyd" else \
         (None, None)
@@ -492,7 +498,8 @@ def main():
             return None, out
     elif native:
         from quantized_channel_estimation_amd.sharding import make_comm
-        comm = make_comm(rank, world, local, kind="rccl")
+        comm_kind = args.comm if args.comm != "auto" else ("host" if world > ndev else "rccl")
+        comm = make_comm(rank, world, local, kind=comm_kind)
         shard = ComponentShardEstimator(means, covs, w, rank, world, device=local, precision=args.precision,
                                         comm=comm, double_buffer=not args.single_buffer)
         dm = shard.dev
@@ -639,8 +646,9 @@ def main():
                        "K": K, "N": N, "B": B, "shard": args.shard,
                        "parallelism": f"{'kshard' if args.shard == 'k' else 'batch'}{world}",
                        "chunks": (args.chunks or default_chunks(world)) if kshard else None,
-                       "collectives": ("libqce RCCL communicator (qce_kshard_*)" if native else
-                                       f"torch.distributed {args.backend}") if kshard else None},
+                       "collectives": (("libqce RCCL communicator (qce_kshard_*)" if comm_kind == "rccl" else
+                                        "libqce host transport over gloo (qce_kshard_*; ranks share a GPU)") if native
+                                       else f"torch.distributed {args.backend}") if kshard else None},
             "mse": mse,
             "parity": parity,
             "roofline": roofline,

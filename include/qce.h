@@ -283,18 +283,21 @@ int qce_kshard_destroy(qce_kshard* ks);
 /* Double-buffered tables: `spare` is a second model of the same shard (same parameters; not owned).  Prepares then
  * alternate between the two table sets on the library's prepare stream: prepare t+1 waits only for the last step
  * that read its set (step t-1), so it runs beside step t's partial kernels (Bussgang_GMM.py:284-287: the next SNR
- * point's tables do not depend on the current estimate); its shift MAX runs on a second (control) communicator. */
+ * point's tables do not depend on the current estimate).  A prepare issues no collective. */
 int qce_kshard_set_spare(qce_kshard* ks, qce_model* spare);
-/* Per-SNR prepare of the shard (qce_prepare) and the shared shift M* = max over ALL components of
- * c_k = -M log(pi) + 2 log det P_k + log w_k (>= every lp: the quad form is >= 0), one MAX all-reduce on `stream`
- * that also carries every rank's Cholesky status (+inf).  No host synchronisation (host transports aside). */
+/* Per-SNR prepare of the shard (qce_prepare) and the shard's shift M_r = max over its components of
+ * c_k = -M log(pi) + 2 log det P_k + log w_k (>= every local lp: the quad form is >= 0; +inf when a Cholesky
+ * factorisation failed).  No collective and no host synchronisation: the shards agree on M* = max_r M_r at the start
+ * of the next qce_kshard_estimate, on the library's communication stream. */
 int qce_kshard_prepare(qce_kshard* ks, const double* A, int M, double snr_db, double n_bits, int quant_kind,
                        const double* thresholds, const double* labels, int n_levels, void* stream);
-/* One estimate step over y (B, M) c128 in device memory (the same y on every rank).
- * QCE_MODE_ALL (gmm_cplx_bussgang.py:220-228): per chunk the shard's shifted FP64 partial rows
- * [s e^{m-M*}, 0, acc e^{m-M*}] (qce_estimate_partial_shifted) and one SUM collective of them on the library's
- * communication stream (reduce-scatter, scatter != 0, or all-reduce), overlapped with the next chunk's kernel;
- * h = acc / s.  QCE_MODE_TOPN / QCE_MODE_CUMP (:197-219, :229-242): n == 1 all-gathers each shard's (max lp, index)
+/* One estimate step over y (B, M) c128 in device memory (the same y on every rank).  Its first collective is an
+ * 8-byte MAX of the shards' shifts M_r (M*); every collective of the library is issued on one communicator from its
+ * communication stream, so all ranks issue them in the same order.
+ * QCE_MODE_ALL (gmm_cplx_bussgang.py:220-228): per chunk the shard's FP64 partial rows [s e^{m-M_r}, 0,
+ * acc e^{m-M_r}] (qce_estimate_partial_shifted) and one SUM collective of them on the communication stream
+ * (reduce-scatter, scatter != 0, or all-reduce) that scales each shard's rows by e^{M_r - M*} on the way in (RCCL
+ * PreMulSum, scalar in device memory), overlapped with the next chunk's kernel; h = acc / s.  QCE_MODE_TOPN / QCE_MODE_CUMP (:197-219, :229-242): n == 1 all-gathers each shard's (max lp, index)
  * and the owner of the first global maximum contributes W_j y + b_j; otherwise the shards' lp are all-gathered,
  * every rank selects the same components (k_select on the full lp) and the shards' weighted filter sums are
  * summed (one chunk).  h_out: device memory, the rows qce_kshard_rows names.  A 2-double MAX of the step's flag
@@ -310,6 +313,9 @@ int qce_kshard_estimate(qce_kshard* ks, const double* y, int64_t B, int mode, do
  * the last step whose shifted sum underflowed are recombined exactly (collective: per-row MAX of the shards'
  * running maxima, then the SUM); QCE_ESTATE if an earlier, already superseded step had such rows. */
 int qce_kshard_finish(qce_kshard* ks, void* stream);
+/* The flag words the last qce_kshard_finish read: [rows of the last step recombined exactly, Cholesky failure on
+ * some rank, the same two for the superseded steps before it] (diagnostics and tests). */
+int qce_kshard_flags(qce_kshard* ks, double* out4);
 /* Kernel timing of the shard's estimate launches (HIP events around each partial / lp launch on the compute
  * stream): enable != 0 starts recording (clears earlier records); qce_kshard_kernel_ms synchronises on the
  * recorded events, returns their summed duration and count, and clears them. */

@@ -98,6 +98,7 @@ SIGNATURES = {
     "qce_kshard_finish": (ctypes.c_int, [_vp, _vp]),
     "qce_kshard_timing": (ctypes.c_int, [_vp, ctypes.c_int]),
     "qce_kshard_kernel_ms": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]),
+    "qce_kshard_flags": (ctypes.c_int, [_vp, _vp]),
 }
 
 # qce_host_collective: int (*)(void* user, int op, const double* send, double* recv, int64_t count)
@@ -550,9 +551,10 @@ class KShard:
             raise ValueError(f"y must have {self.model.M} columns, got {y.shape[1]}")
         check(load().qce_kshard_estimate(self._h, ptr(y), int(B), int(mode), float(param), ch, int(bool(scatter)),
                                          ptr(out), stream))
-        # y and every h since the last finish() stay alive until then: the steps' collectives and row finalisation
-        # may still write h on the library's communication stream
-        self._keep = (self._keep or []) + [(y, out)]
+        # y and h of the steps whose collectives / row finalisation may still run on the library's communication
+        # stream stay alive: the last two (step t+2 waits on the compute stream for step t's communication-stream work,
+        # qce_kshard_estimate), so memory does not grow with the number of steps between finish() calls
+        self._keep = ((self._keep or []) + [(y, out)])[-2:]
         return rows, out
 
     def finish(self, stream=None):
@@ -562,6 +564,13 @@ class KShard:
             check(load().qce_kshard_finish(self._h, stream))
         finally:
             self._keep = None
+
+    def flags(self):
+        """[rows recombined exactly, Cholesky failure, the same for superseded steps] as the last finish() read them
+        (qce_kshard_flags)."""
+        out = np.zeros(4)
+        check(load().qce_kshard_flags(self._h, ptr(out)))
+        return out
 
     def timing(self, enable):
         check(load().qce_kshard_timing(self._h, int(bool(enable))))

@@ -5,9 +5,13 @@
 // the collectives itself -- RCCL over xGMI (ncclAllReduce / ncclReduceScatter / ncclAllGather on device buffers) or
 // a caller-supplied host transport (the library stages through pinned host memory).
 //
-// 'all' mode (gmm_cplx_bussgang.py:220-228): every shard's estimate is written already scaled by the shared,
-// y-independent shift M* = max_k c_k (>= every lp_bk because the quad form is >= 0), so one SUM of the packed rows
-// [s e^{m - M*}, 0, acc e^{m - M*}] over the shards gives h = acc / s.  The batch is cut into chunks; chunk i's
+// 'all' mode (gmm_cplx_bussgang.py:220-228): every shard's estimate is written scaled by its own y-independent
+// shift M_r = max_{k in shard} c_k (>= every local lp_bk because the quad form is >= 0), with no collective between
+// the prepare and the kernel; the step's first collective (an 8-byte MAX on the communication stream) agrees on
+// M* = max_r M_r, and every SUM multiplies the shard's rows by e^{M_r - M*} on the way in (RCCL's PreMulSum with the
+// scalar in device memory; a scaling kernel before a host transport), so one SUM of the packed rows
+// [s e^{m - M*}, 0, acc e^{m - M*}] over the shards gives h = acc / s.  Every collective of the library is issued on
+// one communicator from one stream, so every rank issues them in the same order.  The batch is cut into chunks; chunk i's
 // reduce-scatter runs on the communication stream while chunk i+1's partial kernel runs on the compute stream.
 // Rows whose shifted sum leaves the normal FP64 range are counted on the device; one 2-double MAX per step agrees
 // on the flag word [flagged rows, Cholesky failure], read once at qce_kshard_finish, which recombines the flagged
@@ -173,6 +177,30 @@ __global__ void k_ks_add(double* __restrict__ v, double d) {
   if (threadIdx.x == 0) v[0] += d;
 }
 
+// sh = [M_r, M*] (M* after the MAX): sc = e^{M_r - M*} <= 1, the factor the shard's rows enter the SUM with.  A failed
+// factorisation somewhere (M* = +inf) gives 0 or NaN here; the step's flag word raises before any row is read.
+// bias > 0 (test hook QCE_KSHARD_GLOBAL_BIAS) raises M* so the scaled rows leave the normal range.
+__global__ void k_ks_scale_of(double* __restrict__ sh, double bias, double* __restrict__ sc) {
+  if (threadIdx.x == 0) {
+    sh[1] += bias;
+    sc[0] = exp(sh[0] - sh[1]);
+  }
+}
+
+// test hook QCE_KSHARD_CS_DELAY_US: hold the communication stream for `ticks` of the 100 MHz-class wall clock at the
+// start of a step, so the steps' collectives lag far behind the compute stream (tests of the send-row hand-off)
+__global__ void k_ks_spin(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+}
+
+// host transports: the PreMulSum's multiplication done in place before the rows are staged
+__global__ __launch_bounds__(256) void k_ks_scale_rows(long long n, double* __restrict__ v,
+                                                       const double* __restrict__ sc) {
+  const double f = *sc;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) v[i] *= f;
+}
+
 // first maximum of each lp row (numpy argmax) as (value, index) doubles, one wave per row
 __global__ __launch_bounds__(256) void k_ks_row_argmax(long long B, int K, const double* __restrict__ lp,
                                                        double* __restrict__ out) {
@@ -278,9 +306,7 @@ struct KBuf {
 
 struct qce_comm {
   int rank = 0, world = 1, device = 0, kind = QCE_COMM_RCCL;
-  ncclComm_t nc = nullptr;      // data collectives of the steps (issued only from the K-shard's communication stream)
-  ncclComm_t nc_ctl = nullptr;  // the per-SNR shift MAX (issued only from the prepare stream): a second communicator
-                                // (ncclCommSplit), so the next prepare need not wait for the current step's collectives
+  ncclComm_t nc = nullptr;  // every collective of the K-shard steps, issued only from their communication stream
   qce_host_collective fn = nullptr;
   void* user = nullptr;
   double *pin_send = nullptr, *pin_recv = nullptr;  // host transport staging
@@ -305,10 +331,15 @@ struct qce_kshard {
   KBuf<double> shift, fl, earlier, rs;  // shift: one slot per table set
   KBuf<double> pkb[2];                  // the steps' send rows, alternating: step t+1's kernels fill one while step
   int pkp = 0;                          // t's collectives still read the other
-  KBuf<double> step_shift;              // [parity]: the shift a step used (its flag word reads it on the comm stream)
+  KBuf<double> step_shift;              // [2 parity + 0]: the shard's shift M_r the step's kernels used (copied on the
+                                        // compute stream); [2 parity + 1]: the agreed M* (MAX on the comm stream)
+  KBuf<double> scale;                   // [parity]: e^{M_r - M*}, the PreMulSum scalar of the step's SUMs
+  hipEvent_t ev_pk[2] = {nullptr, nullptr};  // recorded on cs after the last reader of pkb[p] / step_shift[p]
+  int pk_valid[2] = {0, 0};
   hipEvent_t ev_st2cs = nullptr, ev_cs2st = nullptr;
   KBuf<unsigned> cnt;
   double* host_fl = nullptr;  // pinned: [fl0, fl1, earlier0, earlier1] of the last step
+  double last_flags[4] = {0, 0, 0, 0};  // host_fl as the last qce_kshard_finish read it
   int local_chol = 0;         // this rank's library refused a call with the reference's Cholesky error
   // the last step, kept for finish(): exact recombination of flagged rows
   struct {
@@ -335,21 +366,35 @@ int comm_error(const std::string& what, ncclResult_t r) {
   return qce_set_error(QCE_ECOMM, what + " failed: " + ncclGetErrorString(r));
 }
 
-// one collective of doubles on stream st (see the QCE_COLL_* semantics in qce.h)
-int collective(qce_comm* c, int op, const double* send, double* recv, long long count, hipStream_t st,
-               bool ctl = false) {
+// one collective of doubles on stream st (see the QCE_COLL_* semantics in qce.h).  premul (SUM ops only): a device
+// scalar every rank's send data are multiplied by before the sum (ncclRedOpCreatePreMulSum; host transports scale
+// the send buffer in place first).
+int collective(qce_comm* c, int op, double* send, double* recv, long long count, hipStream_t st,
+               const double* premul = nullptr) {
   if (count <= 0) return QCE_OK;
+  const bool sum = op == QCE_COLL_ALLREDUCE_SUM || op == QCE_COLL_REDUCE_SCATTER_SUM;
   if (c->kind == QCE_COMM_RCCL) {
     ncclResult_t r;
-    ncclComm_t nc = ctl ? c->nc_ctl : c->nc;
+    ncclComm_t nc = c->nc;
+    ncclRedOp_t sop = ncclSum;
+    const bool pm = premul && sum;
+    if (pm) {
+      // created per call and destroyed once enqueued (the op is captured at enqueue; the scalar is read on device)
+      r = ncclRedOpCreatePreMulSum(&sop, const_cast<double*>(premul), ncclFloat64, ncclScalarDevice, nc);
+      if (r != ncclSuccess) return comm_error("ncclRedOpCreatePreMulSum", r);
+    }
     switch (op) {
-      case QCE_COLL_ALLREDUCE_SUM: r = ncclAllReduce(send, recv, (size_t)count, ncclFloat64, ncclSum, nc, st); break;
+      case QCE_COLL_ALLREDUCE_SUM: r = ncclAllReduce(send, recv, (size_t)count, ncclFloat64, sop, nc, st); break;
       case QCE_COLL_ALLREDUCE_MAX: r = ncclAllReduce(send, recv, (size_t)count, ncclFloat64, ncclMax, nc, st); break;
       case QCE_COLL_REDUCE_SCATTER_SUM:
-        r = ncclReduceScatter(send, recv, (size_t)count, ncclFloat64, ncclSum, nc, st);
+        r = ncclReduceScatter(send, recv, (size_t)count, ncclFloat64, sop, nc, st);
         break;
       case QCE_COLL_ALLGATHER: r = ncclAllGather(send, recv, (size_t)count, ncclFloat64, nc, st); break;
-      default: return qce_set_error(QCE_EARG, "unknown collective");
+      default: r = ncclInvalidArgument; break;
+    }
+    if (pm) {
+      const ncclResult_t rd = ncclRedOpDestroy(sop, nc);
+      if (r == ncclSuccess && rd != ncclSuccess) return comm_error("ncclRedOpDestroy", rd);
     }
     if (r != ncclSuccess) return comm_error("RCCL collective", r);
     return QCE_OK;
@@ -357,6 +402,10 @@ int collective(qce_comm* c, int op, const double* send, double* recv, long long 
   // host transport: synchronise, stage through pinned memory, call, copy back
   const long long ns = (op == QCE_COLL_REDUCE_SCATTER_SUM) ? count * c->world : count;
   const long long nr = (op == QCE_COLL_ALLGATHER) ? count * c->world : count;
+  if (premul && sum) {
+    hipLaunchKernelGGL(k_ks_scale_rows, dim3(grid_for(ns)), dim3(256), 0, st, ns, send, premul);
+    KS_HIP(hipGetLastError());
+  }
   if ((size_t)ns > c->pin_cap_send) {
     if (c->pin_send) (void)hipHostFree(c->pin_send);
     c->pin_send = nullptr;
@@ -418,7 +467,7 @@ int timed_end(qce_kshard* ks, hipStream_t st) {
 // the SUM collectives of a step's packed rows (pk, W doubles per row) per chunk on the communication stream, each
 // behind its own chunk's producer on `st`, and the rows' finalisation h = acc / s into h_out
 int reduce_chunks(qce_kshard* ks, const std::vector<Chunk>& L, bool scatter, int W, hipStream_t st, double2* h_out,
-                  bool count_flags, size_t chunk_index) {
+                  bool count_flags, size_t chunk_index, const double* premul) {
   qce_comm* c = ks->c;
   const int N = ks->m->N;  // every table set has the same N
   const Chunk& ch = L[chunk_index];
@@ -430,10 +479,10 @@ int reduce_chunks(qce_kshard* ks, const std::vector<Chunk>& L, bool scatter, int
   if (scatter) {
     const long long q = ch.npad / c->world;
     double* recv = ks->rs.p + ch.rs_off * W;
-    KS_RC(collective(c, QCE_COLL_REDUCE_SCATTER_SUM, send, recv, q * W, ks->cs));
+    KS_RC(collective(c, QCE_COLL_REDUCE_SCATTER_SUM, send, recv, q * W, ks->cs, premul));
     rows = recv;
   } else {
-    KS_RC(collective(c, QCE_COLL_ALLREDUCE_SUM, send, send, ch.npad * W, ks->cs));
+    KS_RC(collective(c, QCE_COLL_ALLREDUCE_SUM, send, send, ch.npad * W, ks->cs, premul));
     rows = send;
   }
   if (ch.nv > 0) {
@@ -455,15 +504,19 @@ int ensure_events(qce_kshard* ks, size_t n) {
 
 // close a step: flag word MAX, pinned copy of [fl, earlier], the caller's stream ordered behind the comm stream
 int close_step(qce_kshard* ks) {
-  hipLaunchKernelGGL(k_ks_flags, dim3(1), dim3(64), 0, ks->cs, ks->cnt.p, ks->step_shift.p + ks->pkp, ks->local_chol,
-                     ks->fl.p);
+  hipLaunchKernelGGL(k_ks_flags, dim3(1), dim3(64), 0, ks->cs, ks->cnt.p, ks->step_shift.p + 2 * ks->pkp + 1,
+                     ks->local_chol, ks->fl.p);
   KS_HIP(hipGetLastError());
   KS_RC(collective(ks->c, QCE_COLL_ALLREDUCE_MAX, ks->fl.p, ks->fl.p, 2, ks->cs));
   KS_HIP(hipMemcpyAsync(ks->host_fl, ks->fl.p, 2 * sizeof(double), hipMemcpyDeviceToHost, ks->cs));
   KS_HIP(hipMemcpyAsync(ks->host_fl + 2, ks->earlier.p, 2 * sizeof(double), hipMemcpyDeviceToHost, ks->cs));
   KS_HIP(hipEventRecord(ks->ev_done, ks->cs));  // h_out complete (the caller's stream waits for it in finish)
+  // the last reader of this parity's send rows and shift slots: step t+2 (the next user of the parity) waits for it
+  KS_HIP(hipEventRecord(ks->ev_pk[ks->pkp], ks->cs));
+  ks->pk_valid[ks->pkp] = 1;
   return QCE_OK;
 }
+
 
 // stream hand-offs: every data collective is issued on the communication stream (one stream per communicator)
 int st_to_cs(qce_kshard* ks, hipStream_t st) {
@@ -476,6 +529,20 @@ int cs_to_st(qce_kshard* ks, hipStream_t st) {
   if (st == ks->cs) return QCE_OK;
   KS_HIP(hipEventRecord(ks->ev_cs2st, ks->cs));
   KS_HIP(hipStreamWaitEvent(st, ks->ev_cs2st, 0));
+  return QCE_OK;
+}
+
+// the step's agreed shift on the communication stream: M* = MAX over the shards of M_r (step_shift[2p] -> [2p + 1],
+// after the compute stream's copy of M_r), then the PreMulSum scalar e^{M_r - M*}
+int agree_shift(qce_kshard* ks, hipStream_t st) {
+  double* sh = ks->step_shift.p + 2 * ks->pkp;
+  KS_RC(st_to_cs(ks, st));
+  KS_HIP(hipMemcpyAsync(sh + 1, sh, sizeof(double), hipMemcpyDeviceToDevice, ks->cs));
+  KS_RC(collective(ks->c, QCE_COLL_ALLREDUCE_MAX, sh + 1, sh + 1, 1, ks->cs));
+  double bias = 0.0;
+  if (const char* b = getenv("QCE_KSHARD_GLOBAL_BIAS")) bias = atof(b);  // tests only
+  hipLaunchKernelGGL(k_ks_scale_of, dim3(1), dim3(64), 0, ks->cs, sh, bias, ks->scale.p + ks->pkp);
+  KS_HIP(hipGetLastError());
   return QCE_OK;
 }
 
@@ -526,13 +593,13 @@ int step_all(qce_kshard* ks, qce_model* m, const double2* y, long long B, int ch
       if (!ks->local_chol) {
         KS_RC(timed_begin(ks, st));
         ok = guarded(ks, qce_estimate_partial_shifted(m, reinterpret_cast<const double*>(y + ch.lo * M), n,
-                                                      ks->shift.p + ks->cur, pk, QCE_IO_DEVICE, st), &hard);
+                                                      ks->step_shift.p + 2 * ks->pkp, pk, QCE_IO_DEVICE, st), &hard);
         if (hard) return hard;
         KS_RC(timed_end(ks, st));
       }
       if (!ok) KS_HIP(hipMemsetAsync(pk, 0, sizeof(double) * n * W, st));
     }
-    KS_RC(reduce_chunks(ks, L, scatter, W, st, h, !rowshift, i));
+    KS_RC(reduce_chunks(ks, L, scatter, W, st, h, !rowshift, i, rowshift ? nullptr : ks->scale.p + ks->pkp));
   }
   return QCE_OK;
 }
@@ -664,12 +731,6 @@ int qce_comm_init(const void* unique_id, int rank, int world, int device, qce_co
     delete c;
     return comm_error("ncclCommInitRank", r);
   }
-  r = ncclCommSplit(c->nc, 0, rank, &c->nc_ctl, nullptr);
-  if (r != ncclSuccess) {
-    (void)ncclCommDestroy(c->nc);
-    delete c;
-    return comm_error("ncclCommSplit", r);
-  }
   *out = c;
   return QCE_OK;
 }
@@ -692,7 +753,6 @@ int qce_comm_init_host(int rank, int world, int device, qce_host_collective fn, 
 int qce_comm_destroy(qce_comm* c) {
   if (!c) return QCE_OK;
   DevGuard g(c->device);
-  if (c->nc_ctl) (void)ncclCommDestroy(c->nc_ctl);
   if (c->nc) (void)ncclCommDestroy(c->nc);
   if (c->pin_send) (void)hipHostFree(c->pin_send);
   if (c->pin_recv) (void)hipHostFree(c->pin_recv);
@@ -754,7 +814,9 @@ int qce_kshard_create(qce_model* shard, qce_comm* comm, int K_total, qce_kshard*
   hipError_t e = hipStreamCreateWithFlags(&ks->cs, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ks->ev_done, hipEventDisableTiming);
   if (e == hipSuccess) e = ks->shift.ensure(2);
-  if (e == hipSuccess) e = ks->step_shift.ensure(2);
+  if (e == hipSuccess) e = ks->step_shift.ensure(4);
+  if (e == hipSuccess) e = ks->scale.ensure(2);
+  for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ks->ev_pk[i], hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ks->ev_st2cs, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ks->ev_cs2st, hipEventDisableTiming);
   if (e == hipSuccess) e = ks->fl.ensure(2);
@@ -775,8 +837,9 @@ int qce_kshard_destroy(qce_kshard* ks) {
   if (!ks) return QCE_OK;
   DevGuard g(ks->device);
   if (ks->cs) (void)hipStreamSynchronize(ks->cs);
-  for (auto* b : {&ks->shift, &ks->fl, &ks->earlier, &ks->pkb[0], &ks->pkb[1], &ks->step_shift, &ks->rs, &ks->rm, &ks->rsum, &ks->racc, &ks->mg, &ks->lp,
-                  &ks->lpad, &ks->gath, &ks->lpfull, &ks->wfull, &ks->wloc})
+  for (auto* b : {&ks->shift, &ks->fl, &ks->earlier, &ks->pkb[0], &ks->pkb[1], &ks->step_shift, &ks->scale, &ks->rs,
+                  &ks->rm, &ks->rsum, &ks->racc, &ks->mg, &ks->lp, &ks->lpad, &ks->gath, &ks->lpfull, &ks->wfull,
+                  &ks->wloc})
     b->release();
   ks->cnt.release();
   for (hipEvent_t e : ks->ev_chunk) (void)hipEventDestroy(e);
@@ -788,6 +851,7 @@ int qce_kshard_destroy(qce_kshard* ks) {
   if (ks->ev_st2cs) (void)hipEventDestroy(ks->ev_st2cs);
   if (ks->ev_cs2st) (void)hipEventDestroy(ks->ev_cs2st);
   for (int i = 0; i < 2; ++i) {
+    if (ks->ev_pk[i]) (void)hipEventDestroy(ks->ev_pk[i]);
     if (ks->ev_prep[i]) (void)hipEventDestroy(ks->ev_prep[i]);
     if (ks->ev_used[i]) (void)hipEventDestroy(ks->ev_used[i]);
   }
@@ -826,9 +890,8 @@ int qce_kshard_prepare(qce_kshard* ks, const double* A, int M, double snr_db, do
     KS_HIP(hipMemcpyAsync(shift, &inf, sizeof(double), hipMemcpyHostToDevice, ps));
     KS_HIP(hipStreamSynchronize(ps));
   }
-  // the shift MAX runs on the control communicator, issued only from this stream in prepare order on every rank, so
-  // it need not wait for the previous step's data collectives (their own communicator, their own stream)
-  KS_RC(collective(ks->c, QCE_COLL_ALLREDUCE_MAX, shift, shift, 1, ps, true));
+  // no collective here: the shards agree on M* at the start of the step that uses these tables (agree_shift), on the
+  // communication stream behind the previous step's collectives, so every rank issues its collectives in one order
   if (const char* b = getenv("QCE_KSHARD_SHIFT_BIAS")) {  // tests only: force the underflow path
     hipLaunchKernelGGL(k_ks_add, dim3(1), dim3(64), 0, ps, shift, atof(b));
     KS_HIP(hipGetLastError());
@@ -870,11 +933,20 @@ int qce_kshard_estimate(qce_kshard* ks, const double* y, int64_t B, int mode, do
   double2* hd = reinterpret_cast<double2*>(h_out);
   const bool dbl = ks->mods[1] != nullptr;
   if (dbl) KS_HIP(hipStreamWaitEvent(st, ks->ev_prep[ks->cur], 0));
-  // this step's send rows: the buffer the previous step's collectives do not read; the shift it uses, kept for
-  // its flag word (the next prepare may overwrite the slot before the comm stream gets there)
+  // this step's send rows: the buffer the previous step's collectives do not read, once the step before that (the
+  // last reader of this parity, still in flight on the comm stream) is done with it; the shard's shift, kept in the
+  // parity's slot (the next prepare may overwrite the table set's slot before the comm stream gets there)
   ks->pkp ^= 1;
-  KS_HIP(hipMemcpyAsync(ks->step_shift.p + ks->pkp, ks->shift.p + ks->cur, sizeof(double), hipMemcpyDeviceToDevice,
-                        st));
+  if (ks->pk_valid[ks->pkp]) KS_HIP(hipStreamWaitEvent(st, ks->ev_pk[ks->pkp], 0));
+  KS_HIP(hipMemcpyAsync(ks->step_shift.p + 2 * ks->pkp, ks->shift.p + ks->cur, sizeof(double),
+                        hipMemcpyDeviceToDevice, st));
+  if (const char* d = getenv("QCE_KSHARD_CS_DELAY_US")) {  // tests only
+    int rate_khz = 0;
+    KS_HIP(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, ks->device));
+    hipLaunchKernelGGL(k_ks_spin, dim3(1), dim3(64), 0, ks->cs, (long long)(atof(d) * rate_khz / 1000.0));
+    KS_HIP(hipGetLastError());
+  }
+  KS_RC(agree_shift(ks, st));
   if (B > 0) {
     if (mode == QCE_MODE_ALL) {
       KS_RC(step_all(ks, ks->m, yd, B, chunks, scatter != 0, hd, st, false));
@@ -886,7 +958,7 @@ int qce_kshard_estimate(qce_kshard* ks, const double* y, int64_t B, int mode, do
     KS_HIP(hipEventRecord(ks->ev_used[ks->cur], st));
     ks->used_valid[ks->cur] = 1;
   }
-  KS_RC(st_to_cs(ks, st));  // the flag word reads this step's shift copy
+  KS_RC(st_to_cs(ks, st));  // the flag word closes the step behind its last kernel
   KS_RC(close_step(ks));
   ks->pending.valid = 1;
   ks->pending.y = yd;
@@ -907,6 +979,7 @@ int qce_kshard_finish(qce_kshard* ks, void* stream) {
   hipStream_t st = ks_stream(ks, stream);
   KS_HIP(hipEventSynchronize(ks->ev_done));
   const double f0 = ks->host_fl[0], f1 = ks->host_fl[1], e0 = ks->host_fl[2], e1 = ks->host_fl[3];
+  for (int i = 0; i < 4; ++i) ks->last_flags[i] = ks->host_fl[i];
   auto pend = ks->pending;
   ks->pending.valid = 0;
   ks->any_pending_before = 0;
@@ -926,6 +999,12 @@ int qce_kshard_finish(qce_kshard* ks, void* stream) {
     KS_HIP(hipEventSynchronize(ks->ev_done));
   }
   KS_HIP(hipStreamWaitEvent(st, ks->ev_done, 0));  // the caller's stream sees h complete
+  return QCE_OK;
+}
+
+int qce_kshard_flags(qce_kshard* ks, double* out4) {
+  if (!ks || !out4) return qce_set_error(QCE_EARG, "null argument");
+  for (int i = 0; i < 4; ++i) out4[i] = ks->last_flags[i];
   return QCE_OK;
 }
 

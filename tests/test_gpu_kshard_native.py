@@ -338,3 +338,130 @@ def test_world1_rccl_double_buffered_snr_sweep(rccl1):
     for snr, h in zip(snrs, outs):
         single.prepare(None, snr, 1)
         assert rel_fro(h.cpu().numpy(), single.estimate(np.ascontiguousarray(y))) < 1e-12, snr
+
+
+def test_world1_rccl_premul_scales_rows(rccl1, monkeypatch):
+    """The SUMs take each shard's rows times e^{M_r - M*} (RCCL PreMulSum, scalar in device memory).  At world 1 the
+    factor is 1, so the test hook QCE_KSHARD_GLOBAL_BIAS raises the agreed M* by 2000 nats: the PreMulSum must then
+    zero every row (all of them flagged, flags()[0] == B) and finish() recombines them exactly."""
+    import torch
+    from quantized_channel_estimation_amd import _lib
+    from quantized_channel_estimation_amd.sharding import ComponentShardEstimator
+    fx = load_model("full")
+    y, snr, N, A, n_bits, qtype, quantizer = case_args(fx, str(fx["cases"][0]))
+    Ause = None if np.array_equal(A, np.eye(A.shape[0])) else A
+    qk, thr, lab = _prep_args(n_bits, qtype, quantizer)
+    est = ComponentShardEstimator(fx["means_cplx"], fx["covs_cplx"], fx["weights"], 0, 1, device=0, comm=rccl1)
+    single = _lib.DeviceModel(fx["means_cplx"], fx["covs_cplx"], fx["weights"], device=0)
+    est.prepare(Ause, snr, n_bits, qk, thr, lab)
+    single.prepare(Ause, snr, n_bits, qk, thr, lab)
+    yd = torch.from_numpy(np.ascontiguousarray(y)).cuda()
+    rows, h = est.estimate(yd, chunks=2, scatter=True)
+    assert est.native.flags()[0] == 0.0
+    monkeypatch.setenv("QCE_KSHARD_GLOBAL_BIAS", "2000")
+    rows, h = est.estimate(yd, chunks=2, scatter=True)
+    assert est.native.flags()[0] == y.shape[0]
+    hg, _ = _full_h(rows, h, y.shape[0])
+    assert rel_fro(hg, single.estimate(np.ascontiguousarray(y))) < 1e-12
+
+
+def test_world1_rccl_lagging_comm_stream(rccl1, monkeypatch):
+    """ADVICE r4: the send rows alternate between two buffers, so step t+2 refills the buffer step t's collectives
+    read.  Hold the communication stream 3 ms per step (QCE_KSHARD_CS_DELAY_US) so the collectives lag far behind the
+    compute stream over three sync=False steps at different SNRs, with double-buffered tables: every step's h must
+    still equal the single-GPU result at its SNR (step t+2 waits for step t's communication-stream work)."""
+    import torch
+    from quantized_channel_estimation_amd import _lib
+    from quantized_channel_estimation_amd.sharding import ComponentShardEstimator
+    fx = load_model("fullmean")
+    y, _, N, A, n_bits, qtype, quantizer = case_args(fx, "b1_5")
+    yd = torch.from_numpy(np.ascontiguousarray(y)).cuda()
+    est = ComponentShardEstimator(fx["means_cplx"], fx["covs_cplx"], fx["weights"], 0, 1, device=0, comm=rccl1,
+                                  double_buffer=True)
+    single = _lib.DeviceModel(fx["means_cplx"], fx["covs_cplx"], fx["weights"], device=0)
+    monkeypatch.setenv("QCE_KSHARD_CS_DELAY_US", "3000")
+    snrs = [-10.0, 20.0, 0.0, 10.0]
+    outs = []
+    for snr in snrs:
+        est.prepare(None, snr, 1)
+        rows, h = est.estimate(yd, chunks=2, scatter=False, sync=False)
+        outs.append(h)
+    est.finish()
+    torch.cuda.synchronize()
+    for snr, h in zip(snrs, outs):
+        single.prepare(None, snr, 1)
+        assert rel_fro(h.cpu().numpy(), single.estimate(np.ascontiguousarray(y))) < 1e-12, snr
+
+
+def _interleave_worker(rank, world, port, q):
+    """Two ranks, host transport, double-buffered tables: prepare(t+1) issued between the sync=False estimates t and
+    t+1 on both ranks, one finish at the end."""
+    import sys
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+    from quantized_channel_estimation_amd import _lib
+    from quantized_channel_estimation_amd.sharding import ComponentShardEstimator, make_comm
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=90))
+    torch.cuda.set_device(0)
+    fx = load_model("fullmean")
+    y, _, N, A, n_bits, qtype, quantizer = case_args(fx, "b1_5")
+    yd = torch.from_numpy(np.ascontiguousarray(y)).cuda()
+    comm = make_comm(rank, world, 0, kind="host")
+    est = ComponentShardEstimator(fx["means_cplx"], fx["covs_cplx"], fx["weights"], rank, world, device=0, comm=comm,
+                                  double_buffer=True)
+    single = _lib.DeviceModel(fx["means_cplx"], fx["covs_cplx"], fx["weights"], device=0)
+    snrs = [-10.0, 5.0, 20.0]
+    outs = []
+    est.prepare(None, snrs[0], 1)
+    for i, snr in enumerate(snrs):
+        rows, h = est.estimate(yd, chunks=2, scatter=True, sync=False)
+        outs.append((rows, h))
+        if i + 1 < len(snrs):
+            est.prepare(None, snrs[i + 1], 1)  # the next SNR's tables while this step is in flight
+    est.finish()
+    torch.cuda.synchronize()
+    errs = []
+    for snr, (rows, h) in zip(snrs, outs):
+        single.prepare(None, snr, 1)
+        r = rows.cpu().numpy()
+        errs.append(rel_fro(h.cpu().numpy(), single.estimate(np.ascontiguousarray(y))[r]))
+    est.native.close()
+    comm.close()
+    dist.destroy_process_group()
+    q.put((rank, errs))
+
+
+def test_host_transport_prepare_interleaved_between_async_steps():
+    """VERDICT r4 #2: a prepare between two sync=False estimates on both ranks (double-buffered tables), 2 ranks."""
+    res = _run(_interleave_worker, 2, ())
+    assert sorted(r for r, _ in res) == [0, 1]
+    for rank, errs in res:
+        assert max(errs) < 1e-12, (rank, errs)
+
+
+def test_bench_native_two_ranks_on_one_gpu():
+    """VERDICT r4 #2: the driver's multi-GPU command (bench.py --gpus 2, native backend) end to end on the one-GPU
+    box: launch_ranks, gloo rendezvous, the library's communicator (host transport: the ranks share the GPU),
+    qce_kshard_prepare / estimate / finish with double-buffered tables, MAX-over-ranks timing, teardown.  Metric
+    geometry (K=128, N=M=64) on a 20k batch."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup",
+                        "2", "--batch", "20000", "--cpu-seconds", "0", "--no-extras"], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    r = json.loads(lines[0])
+    assert r["world_size"] == 2 and r["n_gpus"] == 2
+    assert "libqce" in r["config"]["collectives"] and r["config"]["parallelism"] == "kshard2"
+    assert r["parity"]["rel_fro"] < 1e-9
+    assert r["value"] > 0
