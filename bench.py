@@ -303,6 +303,16 @@ def f64_executed_flops(N, K, B):
     return 256.0 * (gl + ntw * kp) * K * B
 
 
+def f64g_executed_flops(N, K, B, has_mean=False):
+    """Executed v_mfma_f64_16x16x4 work of k_est_all_f64g (3M): per component and 16 samples 6 MFMAs per unit of two
+    k-steps and 16-row tile -- GL: 2T + 2 units for tile T (the 16-row triangle), GW: MP / 8 units per tile -- plus
+    2 per tile for the mean / bias columns; 2048 flops per MFMA over 16 samples."""
+    Np = 16 if N <= 16 else (32 if N <= 32 else 64)
+    ntl = ntw = Np // 16
+    mf = 6 * sum(2 * t + 2 for t in range(ntl)) + 6 * (Np // 8) * ntw + (2 * (ntl + ntw) if has_mean else 0)
+    return 2048.0 / 16.0 * mf * K * B
+
+
 def dm_has_mean(dm):
     """Whether the device model carries non-zero means (the bench's synthetic models are zero-mean)."""
     return bool(getattr(dm, "has_mean", False))
@@ -330,23 +340,37 @@ def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
     flops = 16.0 * k_local * N * N * B  # 16 K M N real flops per estimate (dense count)
     if dm.precision == "f64":
         # minimal useful work per (sample, component): the triangular quad form ||Linv y||^2 = M(M+1)/2 complex
-        # MACs (4 M (M+1) real flops) + the filter W y = M N complex MACs (8 M N); with a mean model the -q0
-        # and b columns add 8 M + 8 N.  This is what the kernel has to do, so frac = useful / time / peak <= 1.
-        useful_per = 4.0 * M * (M + 1) + 8.0 * M * N + (8.0 * (M + N) if dm_has_mean(dm) else 0.0)
+        # MACs + the filter W y = M N complex MACs (+ the -q0 and b columns with a mean model).  A complex MAC is
+        # 8 real flops as four real products (the 4M kernel, k_est_all_f64) and 6 as Gauss's three (the 3M kernel,
+        # k_est_all_f64g): frac counts the flops of the algorithm the kernel runs, so it stays <= 1 either way, and
+        # the 4M-equivalent rate (the same work priced at 8 flops per complex MAC) is reported beside it.
+        g3 = dm.kernel() == "f64_3m"
+        cm = 6.0 if g3 else 8.0
+        cmacs = M * (M + 1) / 2.0 + M * N + ((M + N) if dm_has_mean(dm) else 0.0)
+        useful_per = cm * cmacs
         useful = useful_per * k_local * B
         achieved = useful / (kern_ms * 1e-3) / 1e12
         frac = achieved / FP64_MFMA_PEAK_TFLOPS
         assert frac <= 1.0, f"roofline frac {frac:.4f} > 1: the useful-work count or the kernel timing is wrong"
-        kernel = "k_est_all_f64 (+k_merge_f64)" if N <= 128 else "k_lp_f64 + k_wsum_weights + k_wsum_f64"
+        if N > 128:
+            kernel = "k_lp_f64 + k_wsum_weights + k_wsum_f64"
+        else:
+            kernel = ("k_est_all_f64g (3M)" if g3 else "k_est_all_f64") + " (+k_merge_f64)"
         line = dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
                     frac=round(frac, 4), traffic=traffic, kernel=kernel, peak_dtype="fp64 MFMA (dense)",
-                    kernel_ms=round(kern_ms, 4), useful_flops_per_estimate_component=useful_per,
+                    kernel_ms=round(kern_ms, 4), complex_product="3M (Gauss)" if g3 else "4M",
+                    useful_flops_per_estimate_component=useful_per,
                     flops_per_launch=useful, dense_16KMN_flops_per_launch=flops,
-                    note="frac = minimal useful flops (4M(M+1) triangular quad form + 8MN filter per sample and "
-                         "component) / kernel time / FP64 MFMA peak; mfma_issue_frac = executed MFMA flops / "
-                         "time / peak (the pipe occupancy, includes the padding of the 16x16 tiles)")
+                    note=("frac = minimal useful flops of the kernel's algorithm (complex MACs of the triangular quad "
+                          "form M(M+1)/2 + filter MN, x6 real flops as 3M, x8 as 4M) / kernel time / FP64 MFMA peak; "
+                          "mfma_issue_frac = executed MFMA flops / time / peak (the pipe occupancy, includes the "
+                          "padding of the 16x16 tiles)"))
+        if g3:
+            eq = 8.0 * cmacs * k_local * B
+            line["equiv_4m_tflops"] = round(eq / (kern_ms * 1e-3) / 1e12, 3)
+            line["equiv_4m_frac"] = round(eq / (kern_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4)
         if N <= 128:
-            ex = f64_executed_flops(N, k_local, B)
+            ex = f64g_executed_flops(N, k_local, B, dm_has_mean(dm)) if g3 else f64_executed_flops(N, k_local, B)
             line["executed_flops_per_launch"] = ex
             line["mfma_issue_frac"] = round(ex / (kern_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4)
         return line

@@ -146,6 +146,15 @@ int qce_model_info(qce_model* model, int* K, int* N, int* M, int* device);
  * prepared and estimated in the Fourier domain (per-bin tables; fourier_active = 1 after such a prepare).
  * Environment QCE_FFT=0 keeps every prepare on the dense path. */
 int qce_model_structure(qce_model* model, int* n1, int* n2, int* fourier_active);
+/* The 'all'-mode kernel family the last prepare selected (diagnostics, benchmarks): */
+#define QCE_KERNEL_NONE 0     /* not prepared */
+#define QCE_KERNEL_F64_4M 1   /* k_est_all_f64: real 2x2 embedding, FP64 MFMA (padded M, N up to 128) */
+#define QCE_KERNEL_F64_3M 2   /* k_est_all_f64g: Gauss 3-product complex multiply, FP64 MFMA (padded M, N <= 64) */
+#define QCE_KERNEL_F64_WIDE 3 /* k_lp_f64 + k_wsum_f64 (padded 256) */
+#define QCE_KERNEL_BIG 4      /* GEMM path, N or M in (256, 4096] */
+#define QCE_KERNEL_FOURIER 5  /* (block-)circulant models in the Fourier basis */
+#define QCE_KERNEL_FAST 6     /* precision 'fast': fp16 two-term split */
+int qce_model_kernel(qce_model* model, int* kind);
 
 /* Observations on the device (model-free): `get_observation_nbit` (utils.py:241-251) with `quant`
  * (utils.py:189-203):  y = Q(A h + noise_scale * w).
@@ -233,6 +242,12 @@ int qce_rate_bound(const double* h_est, const double* h, int64_t B, int N, const
  * where `io` says; buss (N,) f64, Cq (N,N) c128 and out host; N <= 256; synchronous. */
 int qce_rate_mf(const double* h_est, const double* h, int64_t B, int N, const double* buss, const double* Cq,
                 double* out, int device, int io, void* stream);
+
+/* Page-locked host memory (hipHostMalloc / hipHostFree).  QCE_IO_HOST calls DMA straight from / into page-locked
+ * arrays (and from / into pageable ones they can register for the call): a caller that allocates its result arrays
+ * here, and reuses them, saves the page faults of fresh pageable memory (the Python layer's result pool, _lib.py). */
+int qce_host_alloc(size_t bytes, void** out);
+int qce_host_free(void* p);
 
 /* Device synchronisation of the model's stream (for timing and for QCE_IO_DEVICE callers). */
 int qce_synchronize(qce_model* model);

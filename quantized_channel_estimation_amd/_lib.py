@@ -68,6 +68,9 @@ SIGNATURES = {
     "qce_model_info": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                       ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     "qce_synchronize": (ctypes.c_int, [_vp]),
+    "qce_model_kernel": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
+    "qce_host_alloc": (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    "qce_host_free": (ctypes.c_int, [_vp]),
     "qce_observe": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int, _vp, ctypes.c_int, ctypes.c_double, ctypes.c_int,
                                    _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_double, _vp, _vp, ctypes.c_int, _vp,
                                    ctypes.c_int, ctypes.c_int, _vp]),
@@ -180,6 +183,76 @@ def ptr(a):
     return a.data_ptr()
 
 
+class _PinnedBlock:
+    """A page-locked host allocation (qce_host_alloc); returned to the pool when the last array on it is gone."""
+
+    def __init__(self, nbytes):
+        p = _vp()
+        check(load().qce_host_alloc(int(nbytes), ctypes.byref(p)))
+        self.ptr, self.nbytes = p.value, int(nbytes)
+
+    def __del__(self):
+        try:
+            _pinned_pool.give_back(self)
+        except Exception:
+            pass
+
+
+class _PinnedPool:
+    """Free page-locked blocks kept for reuse (the drop-in numpy API's result arrays): the estimate's D2H lands in
+    them directly, and a block the caller dropped serves the next call without new page faults.  At most
+    `cap_bytes` of free blocks are kept; the rest are freed."""
+
+    def __init__(self, cap_bytes=1 << 30):
+        self.cap = cap_bytes
+        self.free = []  # _PinnedBlock-like records (ptr, nbytes) not referenced by any array
+
+    def take(self, nbytes):
+        best = None
+        for i, (p, n) in enumerate(self.free):
+            if n >= nbytes and n <= 2 * nbytes and (best is None or n < self.free[best][1]):
+                best = i
+        if best is not None:
+            p, n = self.free.pop(best)
+            blk = _PinnedBlock.__new__(_PinnedBlock)
+            blk.ptr, blk.nbytes = p, n
+            return blk
+        return _PinnedBlock(nbytes)
+
+    def give_back(self, blk):
+        if blk.ptr is None:
+            return
+        self.free.append((blk.ptr, blk.nbytes))
+        blk.ptr = None
+        while sum(n for _, n in self.free) > self.cap:
+            p, _ = self.free.pop(0)
+            load().qce_host_free(p)
+
+
+_pinned_pool = _PinnedPool()
+
+
+class _PinnedArrayBase:
+    def __init__(self, blk, shape, dtype):
+        self.blk = blk
+        self.__array_interface__ = {"shape": tuple(shape), "typestr": np.dtype(dtype).str,
+                                    "data": (blk.ptr, False), "version": 3}
+
+
+# results at least this large come from the pinned pool (the size from which QCE_IO_HOST pipelines, 2 x 4096 rows of
+# a 64-wide row); smaller ones are ordinary numpy arrays
+PINNED_MIN_BYTES = 8 << 20
+
+
+def host_empty(shape, dtype=np.complex128):
+    """np.empty((shape), dtype) in page-locked memory from the pool (ordinary numpy array semantics; the block goes
+    back to the pool when the array and its views are gone)."""
+    nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+    if nbytes < PINNED_MIN_BYTES or os.environ.get("QCE_PINNED_RESULTS", "1") == "0":
+        return np.empty(shape, dtype=dtype)
+    return np.asarray(_PinnedArrayBase(_pinned_pool.take(nbytes), shape, dtype))
+
+
 class DeviceModel:
     """Owner of one qce_model handle (device tables of one Gaussian mixture on one GPU)."""
 
@@ -250,7 +323,7 @@ class DeviceModel:
         if io == IO_HOST:
             y = np.ascontiguousarray(y, dtype=np.complex128)
             if out is None:
-                out = np.empty((B, self.N), dtype=np.complex128)
+                out = host_empty((B, self.N), np.complex128)  # the D2H lands in it directly
         elif out is None:
             import torch
             out = torch.empty((B, self.N), dtype=torch.complex128, device=y.device)
@@ -404,6 +477,14 @@ class DeviceModel:
 
     def synchronize(self):
         check(load().qce_synchronize(self._h))
+
+    KERNELS = {0: "none", 1: "f64_4m", 2: "f64_3m", 3: "f64_wide", 4: "big", 5: "fourier", 6: "fast"}
+
+    def kernel(self):
+        """'all'-mode kernel family of the last prepare (qce_model_kernel): f64_3m, f64_4m, fourier, ..."""
+        k = ctypes.c_int()
+        check(load().qce_model_kernel(self._h, ctypes.byref(k)))
+        return self.KERNELS[k.value]
 
     def structure(self):
         """(n1, n2, fourier_active): block-circulant structure found at creation ((0, 0) if none) and

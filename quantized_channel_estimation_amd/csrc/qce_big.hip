@@ -45,7 +45,8 @@ __global__ __launch_bounds__(256) void k_big_lp(long long Bc, int K, int M, cons
   if (lane == 0) lp[b * K + k] = cconst[k] - s;
 }
 
-// weights of one row: mode 1: w = e^{lp - m}, om = m, os = sum w; mode 2: w = e^{lp - shift}, s -> pk[b][0]
+// weights of one row: mode 1: w = e^{lp - m}, om = m, os = sum w; mode 2: w = e^{lp - shift}, s -> pk[b][0];
+// mode 3: the responsibilities w = e^{lp - m} / sum (the 'all' mode's proba for any K, gmm_cplx_bussgang.py:220-228)
 __global__ __launch_bounds__(256) void k_big_weights(long long B, int K, const double* __restrict__ lp, int mode,
                                                      const double* __restrict__ shift, double* __restrict__ w,
                                                      double* __restrict__ om, double* __restrict__ os,
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(256) void k_big_weights(long long B, int K, const d
   if (b >= B) return;
   const double* row = lp + b * K;
   double mx = -__builtin_inf();
-  if (mode == 1) {
+  if (mode != 2) {
     for (int k = lane; k < K; k += 64) mx = fmax(mx, row[k]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
@@ -70,6 +71,11 @@ __global__ __launch_bounds__(256) void k_big_weights(long long B, int K, const d
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (mode == 3) {
+    const double inv = 1.0 / s;
+    for (int k = lane; k < K; k += 64) w[b * K + k] *= inv;
+    return;
+  }
   if (lane == 0) {
     if (mode == 1) {
       om[b] = mx;
@@ -184,6 +190,14 @@ int qce_big_wsum(qce_model* m, const double2* y, long long B, const double* w, d
                        out + r0 * ldo, ldo);
     BIG_HIP(hipGetLastError());
   }
+  return QCE_OK;
+}
+
+// 'all'-mode responsibilities of B rows of lp (m->lp_scr) into m->w64_scr, unbounded K (no LDS-resident row)
+int qce_big_proba(qce_model* m, long long B, hipStream_t st) {
+  hipLaunchKernelGGL(k_big_weights, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, B, m->K, m->lp_scr.p, 3, nullptr,
+                     m->w64_scr.p, nullptr, nullptr, nullptr, 0LL);
+  BIG_HIP(hipGetLastError());
   return QCE_OK;
 }
 

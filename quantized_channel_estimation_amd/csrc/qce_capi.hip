@@ -179,6 +179,8 @@ int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om
     const char* wv = getenv("QCE_F64_WAVES");  // 8 (default): two waves per SIMD where M, N <= 64
     a.waves = (wv && atoi(wv) == 4) ? 4 : 8;
   }
+  a.g3 = m->f64_g3;
+  if (a.g3) a.waves = 8;
 #ifdef QCE_STAMPS
   static unsigned long long* g_stamps = nullptr;
   if (!g_stamps) HIPCHK(hipMalloc(&g_stamps, sizeof(unsigned long long) * 4096 * 8 * 8));
@@ -876,10 +878,17 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
     HIPCHK(qce_launch_pack_wsum(K, M, N, MP, NP, m->has_mean, m->W.p, m->bvec.p,
                                 reinterpret_cast<double*>(m->pack_ws.p), st));
   } else if (m->f64_active) {
-    // FP64 tables of the fused kernel (reference precision)
-    HIPCHK(m->pack_f64.ensure((size_t)qce_pack_f64all_bytes(MP, NP, m->has_mean) * K));
-    HIPCHK(qce_launch_pack_f64all(K, M, N, MP, NP, m->has_mean, m->Linv.p, m->W.p, m->q0.p, m->bvec.p,
+    // FP64 tables of the fused kernel (reference precision): 3M layout where the 3M kernel covers the shape
+    m->f64_g3 = qce_f64g_shape(MP, NP) ? 1 : 0;
+    if (m->f64_g3) {
+      HIPCHK(m->pack_f64.ensure((size_t)qce_pack_f64g_bytes(MP, NP, m->has_mean) * K));
+      HIPCHK(qce_launch_pack_f64g(K, M, N, MP, NP, m->has_mean, m->Linv.p, m->W.p, m->q0.p, m->bvec.p,
                                   reinterpret_cast<double*>(m->pack_f64.p), st));
+    } else {
+      HIPCHK(m->pack_f64.ensure((size_t)qce_pack_f64all_bytes(MP, NP, m->has_mean) * K));
+      HIPCHK(qce_launch_pack_f64all(K, M, N, MP, NP, m->has_mean, m->Linv.p, m->W.p, m->q0.p, m->bvec.p,
+                                    reinterpret_cast<double*>(m->pack_f64.p), st));
+    }
   } else {
     // FP16 two-term split tables; the observation scale makes quantiser outputs exact in fp16
     // (1 bit: y sqrt(2) = +-1; uniform: y 2/delta = odd integers), folded into the slice scales
@@ -955,9 +964,118 @@ long long host_chunk_rows(const qce_model* m, long long B) {
   return (B >= 2 * c) ? c : 0;
 }
 
+// Host memory the GPU can DMA directly: already page-locked (hipHostMalloc'ed, or registered by the caller), or
+// registered here for the duration of one call (hipHostRegister pins the pages the caller's array already has:
+// ~0.3 ms per 100 MB of touched memory, measured on the box, profiles/r05_hostreg_probe.json).
+struct HostDma {
+  void* p = nullptr;
+  bool registered = false;  // registered by this call: unregistered at its end
+  bool ok = false;
+  HostDma(void* ptr, size_t bytes) : p(ptr) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, ptr) == hipSuccess && at.type == hipMemoryTypeHost) {
+      ok = true;
+      return;
+    }
+    (void)hipGetLastError();
+    if (hipHostRegister(ptr, bytes, hipHostRegisterDefault) == hipSuccess) {
+      ok = registered = true;
+      return;
+    }
+    (void)hipGetLastError();  // e.g. a range overlapping another registration: the staged path takes it
+  }
+  ~HostDma() {
+    if (registered) (void)hipHostUnregister(p);
+  }
+};
+
+// row boundaries of the direct-DMA pipeline: chunks growing x4 from the first (whose upload is the only exposed
+// transfer) to the middle and shrinking again (the last chunk's download is the other); an upload of 1 KB rows at
+// ~56 GB/s is ~5x faster than the estimate of a row, so each upload hides behind the previous chunk's kernel
+std::vector<long long> direct_chunks(long long B) {
+  std::vector<long long> sz;
+  const char* e0 = getenv("QCE_HOST_C0");  // first chunk's rows (A/B runs; default B / 24)
+  const char* eg = getenv("QCE_HOST_GROW");  // growth factor of the chunks towards the middle (default 4)
+  long long c0 = e0 ? atoll(e0) : B / 24;
+  const long long grow = eg && atoll(eg) >= 1 ? atoll(eg) : 4;
+  if (c0 < 4096) c0 = 4096;
+  long long left = B;
+  std::vector<long long> head, tail;
+  for (long long c = c0; left > 0;) {
+    if (left <= 2 * c) {
+      head.push_back(left);
+      left = 0;
+      break;
+    }
+    head.push_back(c);
+    tail.push_back(c);
+    left -= 2 * c;
+    c *= grow;
+  }
+  sz = head;
+  for (auto it = tail.rbegin(); it != tail.rend(); ++it) sz.push_back(*it);
+  std::vector<long long> bounds{0};
+  for (long long v : sz) bounds.push_back(bounds.back() + v);
+  return bounds;
+}
+
 }  // namespace
 
 extern "C" {
+
+int qce_host_alloc(size_t bytes, void** out) {
+  if (!out) return fail(QCE_EARG, "null argument");
+  *out = nullptr;
+  HIPCHK(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+  return QCE_OK;
+}
+
+int qce_host_free(void* p) {
+  if (p) HIPCHK(hipHostFree(p));
+  return QCE_OK;
+}
+
+// Host numpy I/O straight from / into the caller's arrays (both DMA-able, see HostDma): per chunk H2D on a copy
+// stream, the estimate on the compute stream, D2H on a second copy stream -- no host copies, one sync at the end.
+static int estimate_host_direct(qce_model* m, const double* y, long long B, int mode, double mode_param,
+                                double* h_out, hipStream_t st) {
+  auto& hp = m->hp;
+  const size_t M = (size_t)m->M, N = (size_t)m->N;
+  if (!hp.s_in) HIPCHK(hipStreamCreateWithFlags(&hp.s_in, hipStreamNonBlocking));
+  if (!hp.s_out) HIPCHK(hipStreamCreateWithFlags(&hp.s_out, hipStreamNonBlocking));
+  for (int i = 0; i < 2; ++i) {
+    if (!hp.ev_in[i]) HIPCHK(hipEventCreateWithFlags(&hp.ev_in[i], hipEventDisableTiming));
+    if (!hp.ev_c[i]) HIPCHK(hipEventCreateWithFlags(&hp.ev_c[i], hipEventDisableTiming));
+  }
+  HIPCHK(m->y_scr.ensure((size_t)B * M));
+  HIPCHK(m->h_scr.ensure((size_t)B * N));
+  const std::vector<long long> bd = direct_chunks(B);
+  const double2* ys = reinterpret_cast<const double2*>(y);
+  double2* hs = reinterpret_cast<double2*>(h_out);
+  // the copy streams start behind the compute stream's earlier work (the scratch buffers' previous readers)
+  HIPCHK(hipEventRecord(hp.ev_c[1], st));
+  HIPCHK(hipStreamWaitEvent(hp.s_in, hp.ev_c[1], 0));
+  int rc = QCE_OK;
+  for (size_t i = 0; i + 1 < bd.size() && rc == QCE_OK; ++i) {
+    const long long o = bd[i], n = bd[i + 1] - bd[i];
+    HIPCHK(hipMemcpyAsync(m->y_scr.p + o * M, ys + o * M, sizeof(double2) * (size_t)n * M, hipMemcpyHostToDevice,
+                          hp.s_in));
+    HIPCHK(hipEventRecord(hp.ev_in[0], hp.s_in));
+    HIPCHK(hipStreamWaitEvent(st, hp.ev_in[0], 0));
+    rc = qce_estimate(m, reinterpret_cast<const double*>(m->y_scr.p + o * M), n, mode, mode_param,
+                      reinterpret_cast<double*>(m->h_scr.p + o * N), QCE_IO_DEVICE, st);
+    if (rc != QCE_OK) break;
+    HIPCHK(hipEventRecord(hp.ev_c[0], st));
+    HIPCHK(hipStreamWaitEvent(hp.s_out, hp.ev_c[0], 0));
+    HIPCHK(hipMemcpyAsync(hs + o * N, m->h_scr.p + o * N, sizeof(double2) * (size_t)n * N, hipMemcpyDeviceToHost,
+                          hp.s_out));
+  }
+  HIPCHK(hipStreamSynchronize(hp.s_in));
+  HIPCHK(hipStreamSynchronize(hp.s_out));
+  if (rc) return rc;
+  HOST_SYNC_CHECK(m, st);
+  return QCE_OK;
+}
 
 // Host numpy I/O split into chunks: host copies into a pinned slot, H2D on a copy stream, the estimate on
 // the compute stream, D2H on a second copy stream into another pinned slot, host copy out -- chunk i's
@@ -1042,8 +1160,15 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
   DeviceGuard g(m->device);
   hipStream_t st = pick_stream(m, stream);
   if (io == QCE_IO_HOST)
-    if (const long long C = host_chunk_rows(m, B))
+    if (const long long C = host_chunk_rows(m, B)) {
+      const char* de = getenv("QCE_HOST_DIRECT");  // QCE_HOST_DIRECT=0: the staged pipeline only (A/B runs, tests)
+      if (!(de && de[0] == '0')) {
+        HostDma dy(const_cast<double*>(y), sizeof(double2) * (size_t)B * m->M);
+        HostDma dh(h_out, sizeof(double2) * (size_t)B * m->N);
+        if (dy.ok && dh.ok) return estimate_host_direct(m, y, B, mode, mode_param, h_out, st);
+      }
       return estimate_host_pipelined(m, y, B, C, mode, mode_param, h_out, st);
+    }
   const double2* dy = nullptr;
   if ((rc = stage_input(m, y, B, io, st, &dy))) return rc;
   double2* dh = reinterpret_cast<double2*>(h_out);
@@ -1067,7 +1192,9 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
     HIPCHK(m->lp_scr.ensure((size_t)B * m->K));
     HIPCHK(m->w64_scr.ensure((size_t)B * m->K));
     if ((rc = qce_big_lp(m, dy, B, m->lp_scr.p, st))) return rc;
-    if (mode == QCE_MODE_ALL)  // responsibilities = proba (:220-228: no renormalisation)
+    if (mode == QCE_MODE_ALL && m->K > qce_select_max_k()) {  // 'all' takes any K
+      if ((rc = qce_big_proba(m, B, st))) return rc;
+    } else if (mode == QCE_MODE_ALL)  // responsibilities = proba (:220-228: no renormalisation)
       HIPCHK(qce_launch_select(B, m->K, m->lp_scr.p, 0, 0, 0.0, m->w64_scr.p, nullptr, nullptr, st));
     else
       HIPCHK(qce_launch_select(B, m->K, m->lp_scr.p, kmode, n, p, nullptr, nullptr, nullptr, st, m->w64_scr.p));
@@ -1413,6 +1540,17 @@ int qce_model_structure(qce_model* m, int* n1, int* n2, int* fourier_active) {
   if (n1) *n1 = m->fft_n1;
   if (n2) *n2 = m->fft_n2;
   if (fourier_active) *fourier_active = m->prepared ? m->fft_active : 0;
+  return QCE_OK;
+}
+
+int qce_model_kernel(qce_model* m, int* kind) {
+  if (!m || !kind) return fail(QCE_EARG, "null argument");
+  if (!m->prepared) *kind = QCE_KERNEL_NONE;
+  else if (m->fft_active) *kind = QCE_KERNEL_FOURIER;
+  else if (m->big) *kind = QCE_KERNEL_BIG;
+  else if (m->f64_active) *kind = m->f64_g3 ? QCE_KERNEL_F64_3M : QCE_KERNEL_F64_4M;
+  else if (m->f64_wide) *kind = QCE_KERNEL_F64_WIDE;
+  else *kind = QCE_KERNEL_FAST;
   return QCE_OK;
 }
 

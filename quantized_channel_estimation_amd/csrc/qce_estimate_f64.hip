@@ -1,6 +1,6 @@
 // FP64 'all'-mode path, host side and the small kernels around k_est_all_f64 (qce_f64_kernel.h):
 // the stream-K merge, the shifted packed partial, table packing and precision conversions.
-#include "qce_f64_kernel.h"
+#include "qce_f64g_kernel.h"
 
 // Combine the stream-K pieces of tiles cut between workgroups (one wave per sample; tiles written
 // whole return at once): h = sum_j acc_j e^{m_j - M} / sum_j s_j e^{m_j - M}, or the merged partial.
@@ -164,12 +164,74 @@ __global__ __launch_bounds__(64) void k_pack_f64all(int M, int N, int MP, int NP
   *reinterpret_cast<double2*>(pack + (((long long)k * bpc + pb) * 64 + lane) * 2) = make_double2(v[0], v[1]);
 }
 
+// 3M tables of k_est_all_f64g (qce_f64g_kernel.h): block j of unit u holds the A operands (Ls, Lm, Lp of the
+// k-steps 2u, 2u + 1 in the order j = 0: Ls s0, Lm s0; 1: Lp s0, Ls s1; 2: Lm s1, Lp s1), Ls = Re + Im, Lm = -2 Im,
+// Lp = 2 Re of the complex entry; lane (r, g) = row 16 T + r, column 4 s + g.  Mean block: (-q0 re, -q0 im) in
+// k = 0; bias block: (b re, b im).
+__global__ __launch_bounds__(64) void k_pack_f64g(int M, int N, int MP, int NP, int has_mean, int bpc,
+                                                  const double2* __restrict__ Linv, const double2* __restrict__ W,
+                                                  const double2* __restrict__ q0, const double2* __restrict__ bvec,
+                                                  double* __restrict__ pack) {
+  const int b = blockIdx.x, k = blockIdx.y, lane = threadIdx.x;
+  const BlockInfo3 bi = block_info3_rt(MP, NP, has_mean ? 1 : 0, b);
+  const int r = lane & 15, gk = lane >> 4;
+  const int i = 16 * bi.T + r;
+  const bool isL = bi.kind <= 1;
+  const int rows = isL ? M : N;
+  double v[2] = {0.0, 0.0};
+  if (bi.kind == 0 || bi.kind == 2) {
+    // (which, k-step) of the block's two MFMAs; which: 0 Ls, 1 Lm, 2 Lp
+    const int s0 = 2 * bi.u, s1 = s0 + 1;
+    const int wh[3][2] = {{0, 1}, {2, 0}, {1, 2}};
+    const int ks[3][2] = {{s0, s0}, {s0, s1}, {s1, s1}};
+    for (int e = 0; e < 2; ++e) {
+      const int j = 4 * ks[bi.j][e] + gk;
+      if (i < rows && j < M) {
+        const double2 z = isL ? Linv[((long long)k * M + i) * M + j] : W[((long long)k * N + i) * M + j];
+        const int which = wh[bi.j][e];
+        v[e] = which == 0 ? z.x + z.y : (which == 1 ? -2.0 * z.y : 2.0 * z.x);
+      }
+    }
+  } else if (bi.kind == 1 && gk == 0 && i < M) {
+    const double2 z = q0[(long long)k * M + i];
+    v[0] = -z.x;
+    v[1] = -z.y;
+  } else if (bi.kind == 3 && gk == 0 && i < N) {
+    const double2 z = bvec[(long long)k * N + i];
+    v[0] = z.x;
+    v[1] = z.y;
+  }
+  *reinterpret_cast<double2*>(pack + (((long long)k * bpc + b) * 64 + lane) * 2) = make_double2(v[0], v[1]);
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 namespace {
 int blocks_per_comp(int MP, int NP, int hm) { return f64_pack_blocks(MP, NP, hm ? 1 : 0); }
+int blocks_per_comp_g(int MP, int NP, int hm) {
+  const int NTL = MP / 16, NTW = NP / 16, KU = MP / 8;
+  const int n = 3 * NTL * (NTL + 1) + hm * NTL + 3 * KU * NTW + hm * NTW;
+  return f64_bpc(n, 0, 1);
+}
 }  // namespace
+
+// the 3M kernel covers padded M, N in {16, 32, 64} (8 waves x 16 samples; QCE_F64_3M=0 keeps the 4M kernel)
+bool qce_f64g_shape(int MP, int NP) {
+  const char* e = getenv("QCE_F64_3M");
+  if (e && e[0] == '0') return false;
+  auto ok = [](int v) { return v == 16 || v == 32 || v == 64; };
+  return ok(MP) && ok(NP);
+}
+long long qce_pack_f64g_bytes(int MP, int NP, int has_mean) { return (long long)blocks_per_comp_g(MP, NP, has_mean) * 1024; }
+hipError_t qce_launch_pack_f64g(int K, int M, int N, int MP, int NP, int has_mean, const double2* Linv,
+                                const double2* W, const double2* q0, const double2* bvec, double* pack,
+                                hipStream_t st) {
+  const int bpc = blocks_per_comp_g(MP, NP, has_mean);
+  hipLaunchKernelGGL(k_pack_f64g, dim3(bpc, K), dim3(64), 0, st, M, N, MP, NP, has_mean, bpc, Linv, W, q0, bvec,
+                     pack);
+  return hipGetLastError();
+}
 
 bool qce_f64_shape(int MP, int NP) {
   auto ok = [](int v) { return v == 16 || v == 32 || v == 64 || v == 128; };
@@ -189,10 +251,19 @@ hipError_t qce_launch_pack_f64all(int K, int M, int N, int MP, int NP, int has_m
 
 template <int MP>
 hipError_t qce_f64_launch_mp(const QceF64Args& a, bool out_partial, hipStream_t st);
+template <int MP>
+hipError_t qce_f64g_launch_mp(const QceF64Args& a, bool out_partial, hipStream_t st);
 
 hipError_t qce_launch_est_f64(const QceF64Args& a, bool out_partial, hipStream_t st) {
   hipError_t e;
-  switch (a.MP) {
+  if (a.g3) {
+    switch (a.MP) {
+      case 16: e = qce_f64g_launch_mp<16>(a, out_partial, st); break;
+      case 32: e = qce_f64g_launch_mp<32>(a, out_partial, st); break;
+      case 64: e = qce_f64g_launch_mp<64>(a, out_partial, st); break;
+      default: e = hipErrorInvalidValue;
+    }
+  } else switch (a.MP) {
     case 16: e = qce_f64_launch_mp<16>(a, out_partial, st); break;
     case 32: e = qce_f64_launch_mp<32>(a, out_partial, st); break;
     case 64: e = qce_f64_launch_mp<64>(a, out_partial, st); break;

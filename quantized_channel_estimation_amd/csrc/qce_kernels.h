@@ -103,7 +103,13 @@ struct QceF64Args {
   const double* shift = nullptr;  // device pointer: the shared shift M* of the packed partial
   unsigned long long* stamps = nullptr;  // diagnostic builds (-DQCE_STAMPS): per-wave segment cycles
   int waves = 8;  // workgroup shape where M, N <= 64: 8 waves x 1 column tile (two per SIMD), or 4 x 2 (QCE_F64_WAVES=4)
+  int g3 = 0;     // 3M tables / kernel (k_est_all_f64g, padded M, N <= 64; always 8 waves x 16 samples)
 };
+bool qce_f64g_shape(int MP, int NP);
+long long qce_pack_f64g_bytes(int MP, int NP, int has_mean);
+hipError_t qce_launch_pack_f64g(int K, int M, int N, int MP, int NP, int has_mean, const double2* Linv,
+                                const double2* W, const double2* q0, const double2* bvec, double* pack,
+                                hipStream_t st);
 bool qce_f64_shape(int MP, int NP);
 int qce_f64_tile(int MP, int NP);  // samples per workgroup tile
 long long qce_pack_f64all_bytes(int MP, int NP, int has_mean);

@@ -66,6 +66,7 @@ struct qce_model {
   DevBuf<int> yflag;
   // FP64 fused-kernel tables (qce_estimate_f64.hip) and its cut-tile scratch
   DevBuf<char> pack_f64;
+  int f64_g3 = 0;  // pack_f64 holds the 3M layout (k_est_all_f64g)
   int f64_active = 0;  // the last dense prepare packed FP64 tables: 'all' / partial run k_est_all_f64
   DevBuf<char> pack_ws;
   int f64_wide = 0;    // ... or, beyond padded 128, the two-pass FP64 path (qce_wsum_f64.hip)
@@ -116,6 +117,7 @@ int qce_weighted_estimate(qce_model* m, const double2* y, long long B, const dou
 // qce_big.hip: the GEMM-based FP64 path for N or M in (256, QCE_BIG_MAX]
 #define QCE_BIG_MAX 4096
 int qce_big_lp(qce_model* m, const double2* y, long long B, double* lp, hipStream_t st);
+int qce_big_proba(qce_model* m, long long B, hipStream_t st);
 int qce_big_wsum(qce_model* m, const double2* y, long long B, const double* w, double2* out, long long ldo,
                  hipStream_t st);
 int qce_big_partial(qce_model* m, const double2* y, long long B, int wmode, double* om, double* os, double* oa,

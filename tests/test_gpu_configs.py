@@ -212,3 +212,22 @@ def test_wide_dimensions_all_modes(N, pilots, K, with_mean):
     one = np.ones(2)
     with pytest.raises(NotImplementedError):  # beyond QCE_BIG_MAX: refused before any upload
         _lib.check(_lib.load().qce_model_create(1, 4097, None, _lib.ptr(one), _lib.ptr(one), 0, ctypes.byref(h)))
+
+
+def test_wide_dimensions_all_mode_beyond_select_k():
+    """'all' mode on the GEMM path (N > 256) with K beyond the selection kernels' K (4096) takes its
+    responsibilities from a K-unbounded row kernel.  Mixture of 5 distinct components, each repeated 820 times
+    (K = 4100) with its weight split evenly: the estimate equals the 5-component mixture's (FP64 oracle, 1e-9)."""
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import _lib, inputs
+    N, Kd, rep = 264, 5, 820
+    means, covs, w = inputs.synthetic_model(Kd, N, seed=5)
+    assert Kd * rep > 4096  # qce_select_max_k (k_select_wide)
+    rng = np.random.default_rng(6)
+    y = (np.sign(rng.standard_normal((32, N))) + 1j * np.sign(rng.standard_normal((32, N)))) / np.sqrt(2)
+    dm = _lib.DeviceModel(np.repeat(means, rep, axis=0), np.repeat(covs, rep, axis=0), np.repeat(w / rep, rep))
+    dm.prepare(None, 5.0, 1.0)
+    h = dm.estimate(y, _lib.MODE_ALL, 0.0)
+    ho = O.estimate(means, covs, w, y, 5.0, N, None, "all", 1)
+    assert rel_fro(h, ho) < 1e-9, rel_fro(h, ho)
+    dm.close()

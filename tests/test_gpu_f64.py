@@ -227,3 +227,39 @@ def test_f64_selective_modes_vs_oracle(K, N, pilots, B, n_bits, mean):
         hg = g.estimate_from_y(y, 5.0, N, A, mode, n_bits, "uniform", qz)
         ho = O.estimate(means, covs, w, y, 5.0, N, A, mode, n_bits, "uniform", qz)
         assert rel_fro(hg, ho) < tol, (mode, rel_fro(hg, ho))
+
+
+@pytest.mark.parametrize("N,M_pilots,mean", [(64, 1, False), (64, 1, True), (48, 1, True), (32, 1, False),
+                                             (16, 1, True), (20, 1, False), (32, 2, True), (16, 4, False)])
+def test_f64_3m_matches_4m_and_oracle(N, M_pilots, mean, monkeypatch):
+    """The 3M (Gauss) kernel k_est_all_f64g against the 4M kernel k_est_all_f64 (QCE_F64_3M=0 at prepare) and the FP64
+    oracle: same FP64 computation up to rounding (1e-12 relative between the kernels, 1e-9 vs the oracle), for every
+    padded shape it covers (M, N in {16, 32, 64}, square and with pilots M = 2N, 4N), with and without means, and the
+    stream-K partial / K-shard packed outputs."""
+    _gpu_or_skip()
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import _lib
+    K, B = 24, 1500
+    means, covs, w, h, _, _ = _synthetic(K, N, B, 500 + N, 1, mean=mean)
+    rng = np.random.default_rng(N + M_pilots)
+    M = N * M_pilots
+    A = None if M_pilots == 1 else np.kron(np.exp(2j * np.pi * rng.random((M_pilots, 1))), np.eye(N)) / np.sqrt(M_pilots)
+    y = (np.sign(rng.standard_normal((B, M))) + 1j * np.sign(rng.standard_normal((B, M)))) / np.sqrt(2)
+    dm = _lib.DeviceModel(means, covs, w)
+    dm.prepare(A, 5.0, 1.0)
+    assert dm.kernel() == "f64_3m"
+    h3 = dm.estimate(y)
+    m3, s3, a3 = dm.partial64(y)
+    monkeypatch.setenv("QCE_F64_3M", "0")
+    dm.prepare(A, 5.0, 1.0)
+    assert dm.kernel() == "f64_4m"
+    h4 = dm.estimate(y)
+    m4, s4, a4 = dm.partial64(y)
+    assert rel_fro(h3, h4) < 1e-12, rel_fro(h3, h4)
+    sc = np.exp(m3 - m4)  # the lazy running maxima may settle on different components
+    assert rel_fro(a3 * sc[:, None], a4) < 1e-12 and rel_fro(s3 * sc, s4) < 1e-12
+    Ao = np.eye(N) if A is None else A
+    ho = O.estimate(means, covs, w, y, 5.0, N, Ao, "all", 1)
+    tol = F64_TOL if M_pilots == 1 else 1e-6  # 1 bit with a general A: the arcsine law's documented sensitivity
+    assert rel_fro(h3, ho) < tol, rel_fro(h3, ho)
+    dm.close()
