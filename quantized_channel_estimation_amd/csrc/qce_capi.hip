@@ -133,9 +133,10 @@ bool want_f64(const qce_model* m) {
 // (m, s, acc) partial when h == nullptr (K-shard path)
 int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, double* oa,
             hipStream_t st, double* pk = nullptr, const double* shift = nullptr) {
-  const long long TS = qce_f64_tile(m->MP, m->NP);
+  const long long TS = m->f64_g3 ? 16LL * qce_f64g_waves() : qce_f64_tile(m->MP, m->NP);
   const long long tiles = (B + TS - 1) / TS;
-  long long slots = m->cu_count;  // 128 KB of LDS: one workgroup per CU
+  // one 8-wave workgroup per CU (its ring fills the LDS), or two 4-wave ones (3M kernel built with 4 waves)
+  long long slots = (long long)m->cu_count * (m->f64_g3 ? 8 / qce_f64g_waves() : 1);
   const char* e = getenv("QCE_WORKGROUPS");
   if (e && atoll(e) > 0) slots = atoll(e);
   long long nwg, R, L;
@@ -180,7 +181,7 @@ int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om
     a.waves = (wv && atoi(wv) == 4) ? 4 : 8;
   }
   a.g3 = m->f64_g3;
-  if (a.g3) a.waves = 8;
+  if (a.g3) a.waves = qce_f64g_waves();
 #ifdef QCE_STAMPS
   static unsigned long long* g_stamps = nullptr;
   if (!g_stamps) HIPCHK(hipMalloc(&g_stamps, sizeof(unsigned long long) * 4096 * 8 * 8));

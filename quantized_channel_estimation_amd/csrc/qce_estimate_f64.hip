@@ -209,11 +209,7 @@ __global__ __launch_bounds__(64) void k_pack_f64g(int M, int N, int MP, int NP, 
 // ---------------------------------------------------------------------------
 namespace {
 int blocks_per_comp(int MP, int NP, int hm) { return f64_pack_blocks(MP, NP, hm ? 1 : 0); }
-int blocks_per_comp_g(int MP, int NP, int hm) {
-  const int NTL = MP / 16, NTW = NP / 16, KU = MP / 8;
-  const int n = 3 * NTL * (NTL + 1) + hm * NTL + 3 * KU * NTW + hm * NTW;
-  return f64_bpc(n, 0, 1);
-}
+int blocks_per_comp_g(int MP, int NP, int hm) { return f64g_bpc(f64g_blocks(MP, NP, hm ? 1 : 0)); }
 }  // namespace
 
 // the 3M kernel covers padded M, N in {16, 32, 64} (8 waves x 16 samples; QCE_F64_3M=0 keeps the 4M kernel)
@@ -223,6 +219,7 @@ bool qce_f64g_shape(int MP, int NP) {
   auto ok = [](int v) { return v == 16 || v == 32 || v == 64; };
   return ok(MP) && ok(NP);
 }
+int qce_f64g_waves() { return QCE_F64G_NW; }
 long long qce_pack_f64g_bytes(int MP, int NP, int has_mean) { return (long long)blocks_per_comp_g(MP, NP, has_mean) * 1024; }
 hipError_t qce_launch_pack_f64g(int K, int M, int N, int MP, int NP, int has_mean, const double2* Linv,
                                 const double2* W, const double2* q0, const double2* bvec, double* pack,
@@ -271,7 +268,7 @@ hipError_t qce_launch_est_f64(const QceF64Args& a, bool out_partial, hipStream_t
     default: e = hipErrorInvalidValue;
   }
   if (e != hipSuccess) return e;
-  const long long TS = qce_f64_tile(a.MP, a.NP);
+  const long long TS = a.g3 ? 16LL * QCE_F64G_NW : qce_f64_tile(a.MP, a.NP);
   const long long tiles = (a.B + TS - 1) / TS;
   const long long tail0 = (long long)a.R * a.nwg;
   if (a.L > 0 && tiles > tail0) {  // some tail tile may be cut between workgroups

@@ -39,10 +39,56 @@
 // LDS operand prefetch distance (blocks).  Smaller than the 4M kernel's 8: the three accumulator sets of the filter
 // take the registers (E = 4..8 were within 0.5 % of each other on the 4M kernel, profiles/r04_f64_prefetch_ab2.txt).
 #ifndef QCE_F64G_E
-#define QCE_F64G_E 3
+#define QCE_F64G_E 2
+#endif
+// waves per workgroup: 8 (one 8-wave workgroup per CU, two waves per SIMD, one ring of <= 144 KB) or 4 (two
+// 4-wave workgroups per CU, each with its own ring of <= 72 KB: a workgroup's ring barriers then sync one wave per
+// SIMD, the other workgroup's wave keeps the SIMD's MFMA pipe busy)
+#ifndef QCE_F64G_NW
+#define QCE_F64G_NW 8
+#endif
+// ring chunk (blocks); 0 = chosen from the block count (f64_cb)
+#ifndef QCE_F64G_CB
+#define QCE_F64G_CB 0
+#endif
+// 1: libm exp for the softmax weights (A/B builds)
+#ifndef QCE_F64G_LIBM_EXP
+#define QCE_F64G_LIBM_EXP 0
 #endif
 
 namespace {
+
+// e^x for x <= 700 with a 32-entry LDS table of 2^(j/32) and a degree-6 polynomial of e^r, |r| <= ln 2 / 64
+// (truncation 4e-18, about 2 ulp): 18 VALU and four non-inline constants against libm's ~32 instructions and
+// ~13 constants that the compiler keeps in VGPRs across the component loop (they spilled beside the 3M kernel's
+// accumulators).  x = -inf and x < -708 give e^-708 = 3e-308, negligible beside the softmax's largest weight 1.
+QCE_DEV double exp_tab64(double x, const double* __restrict__ tab) {
+  constexpr double L32 = 46.166241308446828384;     // 32 / ln 2
+  constexpr double LH = 2.1660849390173098072e-02;  // ln 2 / 32, leading bits
+  constexpr double LL = 2.3251928468788740148e-12;  // ln 2 / 32 - LH
+  x = fmax(x, -708.0);
+  const double kf = __builtin_rint(x * L32);
+  double r = fma(kf, -LH, x);
+  r = fma(kf, -LL, r);
+  const int k = (int)kf;
+  double p = fma(r, 1.0 / 720.0, 1.0 / 120.0);
+  p = fma(p, r, 1.0 / 24.0);
+  p = fma(p, r, 1.0 / 6.0);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  const double v = tab[k & 31] * p;
+  return __hiloint2double(__double2hiint(v) + ((k >> 5) << 20), __double2loint(v));
+}
+
+// ring chunk (blocks) and padded blocks per component of the 3M table: shared by the kernel and k_pack_f64g
+constexpr __host__ __device__ int f64g_cb(int blocks) {
+  return QCE_F64G_CB > 0 ? QCE_F64G_CB : (QCE_F64G_NW == 8 ? f64_cb(blocks, 0, 1) : 24);
+}
+constexpr __host__ __device__ int f64g_bpc(int blocks) { return (blocks + f64g_cb(blocks) - 1) / f64g_cb(blocks) * f64g_cb(blocks); }
+constexpr __host__ __device__ int f64g_blocks(int MP, int NP, int hmi) {
+  return 3 * (MP / 16) * (MP / 16 + 1) + hmi * (MP / 16) + 3 * (MP / 8) * (NP / 16) + hmi * (NP / 16);
+}
 
 template <int MP, int NP, bool HM>
 struct F64G3 {
@@ -56,10 +102,13 @@ struct F64G3 {
   static constexpr int GL_BLOCKS = gl_off(NTL);
   static constexpr int GW_BLOCKS = 3 * KU * NTW + HMI * NTW;
   static constexpr int BLOCKS = GL_BLOCKS + GW_BLOCKS;
-  static constexpr int CB = f64_cb(BLOCKS, 0, 1);  // blocks per ring chunk
-  static constexpr int NSLOT = f64_nslot(CB);
+  static constexpr int NWG = QCE_F64G_NW;  // waves per workgroup
+  static constexpr int LDS_KB = NWG == 8 ? 144 : 72;
+  static constexpr int CB = f64g_cb(BLOCKS);
+  static constexpr int NSLOT = LDS_KB / CB < 8 ? LDS_KB / CB : 8;
   static constexpr int CHUNK = CB * 1024;
-  static constexpr int BPC = f64_bpc(BLOCKS, 0, 1);
+  static constexpr int BPC = f64g_bpc(BLOCKS);
+  static_assert(BLOCKS == f64g_blocks(MP, NP, HMI), "block count");
   static constexpr int CPC = BPC / CB;
 };
 
@@ -90,7 +139,7 @@ __host__ __device__ constexpr BlockInfo3 block_info3_rt(int MP, int NP, int hmi,
 }  // namespace
 
 template <int MP, int NP, bool HM, bool OUT_PARTIAL>
-__global__ __launch_bounds__(512) void k_est_all_f64g(long long B, int M, int N, int K, int R, long long L,
+__global__ __launch_bounds__(QCE_F64G_NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_est_all_f64g(long long B, int M, int N, int K, int R, long long L,
                                                       const double2* __restrict__ y, const char* __restrict__ pack,
                                                       const double* __restrict__ cconst, double2* __restrict__ h,
                                                       double* __restrict__ om, double* __restrict__ os,
@@ -99,18 +148,21 @@ __global__ __launch_bounds__(512) void k_est_all_f64g(long long B, int M, int N,
                                                       double* __restrict__ pk, const double* __restrict__ shift,
                                                       unsigned long long* __restrict__ stamps) {
   using G = F64G3<MP, NP, HM>;
-  constexpr int NW = 8;           // waves: two per SIMD, 16 samples each
+  constexpr int NW = G::NWG;       // waves of 16 samples; two per SIMD (one or two workgroups per CU)
   constexpr int TS = NW * 16;     // samples per tile
   constexpr int LPW = G::CB / NW;  // global_load_lds pieces per wave per chunk
   constexpr int E = QCE_F64G_E;
   constexpr double RESCALE = 32.0;  // lazy max: rescale only when lp exceeds m by this
   static_assert(G::CB % NW == 0, "chunk split");
   static_assert(E < G::CB, "the prefetch window must stay inside one chunk");
+  static_assert(G::NSLOT >= 3, "ring depth");
   __shared__ __attribute__((aligned(16))) char lds[G::NSLOT * G::CHUNK];
+  __shared__ double etab[32];  // 2^(j/32) for exp_tab64
 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int g = lane >> 4, col = lane & 15;
+  if (threadIdx.x < 32) etab[threadIdx.x] = exp2((double)threadIdx.x / 32.0);  // visible after the first barrier
   const long long P = gridDim.x, w = blockIdx.x;
   const long long tiles = (B + TS - 1) / TS;
   const long long tail0 = (long long)R * P;
@@ -300,7 +352,8 @@ __global__ __launch_bounds__(512) void k_est_all_f64g(long long B, int M, int N,
               gap();
             }
             if constexpr (RB && NMF == 0) refill_pieces(0, LPW);
-            // end of a GL row tile: |z|^2 of its 16 complex rows into the lane's quad-form partial
+            // end of a GL row tile: |z|^2 of its 16 complex rows into the lane's quad-form partial (folding one block
+            // later, after the next tile's first MFMAs, measured 1 % slower: the extra live accumulators spill)
             if constexpr (bi.kind == 0 || bi.kind == 1) {
               constexpr bool last =
                   HM ? (bi.kind == 1) : (bi.u == G::gl_units(bi.T) - 1 && bi.j == 2);
@@ -332,7 +385,11 @@ __global__ __launch_bounds__(512) void k_est_all_f64g(long long B, int M, int N,
                   oi[T] *= al;
                 }
               }
+#if QCE_F64G_LIBM_EXP
               p = (lp == QCE_NEG_INF) ? 0.0 : exp(lp - m);
+#else
+              p = (lp == QCE_NEG_INF) ? 0.0 : exp_tab64(lp - m, etab);
+#endif
               ssum += p;
               F64_STAMP(1);
             }
@@ -402,7 +459,7 @@ __global__ __launch_bounds__(512) void k_est_all_f64g(long long B, int M, int N,
 
 template <int MP, int NP, bool HM, bool OP>
 hipError_t qce_f64g_launch_t(const QceF64Args& a, hipStream_t st) {
-  hipLaunchKernelGGL((k_est_all_f64g<MP, NP, HM, OP>), dim3((unsigned)a.nwg), dim3(512), 0, st, a.B, a.M, a.N, a.K,
+  hipLaunchKernelGGL((k_est_all_f64g<MP, NP, HM, OP>), dim3((unsigned)a.nwg), dim3(QCE_F64G_NW * 64), 0, st, a.B, a.M, a.N, a.K,
                      a.R, a.L, a.y, a.pack, a.cconst, a.h, a.om, a.os, a.oa, a.pm, a.ps, a.pa, a.pk, a.shift,
                      a.stamps);
   return hipGetLastError();

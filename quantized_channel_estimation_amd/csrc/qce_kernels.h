@@ -106,6 +106,7 @@ struct QceF64Args {
   int g3 = 0;     // 3M tables / kernel (k_est_all_f64g, padded M, N <= 64; always 8 waves x 16 samples)
 };
 bool qce_f64g_shape(int MP, int NP);
+int qce_f64g_waves();  // waves per workgroup of k_est_all_f64g (tile = 16 x waves samples; 8 / waves workgroups per CU)
 long long qce_pack_f64g_bytes(int MP, int NP, int has_mean);
 hipError_t qce_launch_pack_f64g(int K, int M, int N, int MP, int NP, int has_mean, const double2* Linv,
                                 const double2* W, const double2* q0, const double2* bvec, double* pack,
