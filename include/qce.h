@@ -58,6 +58,9 @@ typedef struct qce_model qce_model;
                                ~1e-7 relative; an opt-in throughput mode) */
 #define QCE_PRECISION_F64 0
 #define QCE_PRECISION_FAST 1
+#define QCE_OPT_RESERVE_CUS 3 /* CUs the persistent estimate kernels leave free (value >= 0; default 0): room for the
+                                 collective kernels of a concurrent communication stream (qce_kshard_create sets it on
+                                 the shard's models for RCCL at world > 1).  Keeps the prepared state. */
 
 #define QCE_IO_HOST 0
 #define QCE_IO_DEVICE 1

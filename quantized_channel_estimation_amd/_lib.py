@@ -15,6 +15,7 @@ QCE_OK, QCE_EARG, QCE_ECHOL, QCE_ENOTIMPL, QCE_EHIP, QCE_ESTATE, QCE_ECOMM = ran
 MODE_ALL, MODE_TOPN, MODE_CUMP = 0, 1, 2
 OPT_BETA_FIRST = 1
 OPT_PRECISION = 2
+OPT_RESERVE_CUS = 3
 PRECISION_F64, PRECISION_FAST = 0, 1
 QUANT_UNIFORM, QUANT_LLOYD, QUANT_OTHER = 0, 1, 2
 IO_HOST, IO_DEVICE = 0, 1
@@ -441,6 +442,11 @@ class DeviceModel:
         val = {"f64": PRECISION_F64, "fast": PRECISION_FAST}[precision]
         self.set_option(OPT_PRECISION, val)
         self.precision = precision
+
+    def reserve_cus(self, n):
+        """CUs the persistent estimate kernels leave free for a concurrent communication stream (QCE_OPT_RESERVE_CUS;
+        the prepared tables stay valid)."""
+        check(load().qce_model_set_option(self._h, OPT_RESERVE_CUS, float(n)))
 
     def set_option(self, option, value):
         check(load().qce_model_set_option(self._h, int(option), float(value)))

@@ -136,7 +136,7 @@ int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om
   const long long TS = m->f64_g3 ? 16LL * qce_f64g_waves() : qce_f64_tile(m->MP, m->NP);
   const long long tiles = (B + TS - 1) / TS;
   // one 8-wave workgroup per CU (its ring fills the LDS), or two 4-wave ones (3M kernel built with 4 waves)
-  long long slots = (long long)m->cu_count * (m->f64_g3 ? 8 / qce_f64g_waves() : 1);
+  long long slots = (long long)m->sched_cus() * (m->f64_g3 ? 8 / qce_f64g_waves() : 1);
   const char* e = getenv("QCE_WORKGROUPS");
   if (e && atoll(e) > 0) slots = atoll(e);
   long long nwg, R, L;
@@ -243,7 +243,7 @@ int run_h2(qce_model* m, const double2* dy, long long B, double2* h, double* om,
            hipStream_t st) {
   if (qce_h2x_shape(m->MP, m->NP)) return run_h2x(m, dy, B, h, om, os, oa, st);
   const long long tiles = (B + 255) / 256;
-  long long slots = (long long)m->cu_count * qce_h2_blocks_per_cu(m->MP, m->NP, m->has_mean);
+  long long slots = (long long)m->sched_cus() * qce_h2_blocks_per_cu(m->MP, m->NP, m->has_mean);
   const char* e = getenv("QCE_WORKGROUPS");
   if (e && atoll(e) > 0) slots = atoll(e);
   // data-parallel rounds of whole tiles, stream-K over the remaining tiles' (tile, component) items
@@ -298,7 +298,7 @@ int run_h2x(qce_model* m, const double2* dy, long long B, double2* h, double* om
             hipStream_t st) {
   const long long tiles = (B + qce_h2x_tile() - 1) / qce_h2x_tile();
   const long long nrc = qce_h2x_row_chunks(m->MP, m->NP);
-  const long long slots = m->cu_count;  // one 128 KB-LDS workgroup per CU
+  const long long slots = m->sched_cus();  // one 128 KB-LDS workgroup per CU
   int ksplit = 1;
   double best = 0.0;
   for (int s = 1; s <= 8 && s <= m->K; ++s) {  // fill the chip: tiles*s*nrc over whole waves of workgroups
@@ -412,7 +412,7 @@ QceFftEstArgs fft_args(qce_model* m, const double2* y, long long B) {
   a.pw = m->f_pw.p;
   a.pbr = m->f_pbr.p;
   a.pbi = m->f_pbi.p;
-  a.cu = m->cu_count;
+  a.cu = m->sched_cus();
   a.chunk = m->fft_chunk;
   return a;
 }
@@ -1782,6 +1782,11 @@ int qce_model_set_option(qce_model* m, int option, double value) {
   if (option == QCE_OPT_BETA_FIRST) {
     m->beta_first = value != 0.0;
     m->prepared = 0;
+    return QCE_OK;
+  }
+  if (option == QCE_OPT_RESERVE_CUS) {
+    if (value < 0.0 || value != floor(value)) return fail(QCE_EARG, "reserve_cus must be an integer >= 0");
+    m->reserve_cus = value > 1e6 ? 1000000 : (int)value;
     return QCE_OK;
   }
   if (option == QCE_OPT_PRECISION) {

@@ -117,6 +117,15 @@ std::vector<Chunk> chunk_layout(long long B, int chunks, int world, int rank, bo
   return out;
 }
 
+// CUs the shard's persistent estimate kernels leave free for the step's RCCL kernels (QCE_KSHARD_RESERVE_CUS,
+// default 16 = two per XCD): the grid otherwise holds every CU with one 144 KB-LDS, full-VGPR workgroup, so a
+// reduce-scatter of step t could not start before step t+1's kernel ended; with the reservation it runs beside it
+int kshard_reserve_cus() {
+  const char* e = getenv("QCE_KSHARD_RESERVE_CUS");
+  const int v = e ? atoi(e) : 16;
+  return v < 0 ? 0 : v;
+}
+
 void slice_of(int K, int world, int rank, int* lo, int* hi) {
   const int base = K / world, rem = K % world;
   *lo = rank * base + (rank < rem ? rank : rem);
@@ -802,6 +811,7 @@ int qce_kshard_create(qce_model* shard, qce_comm* comm, int K_total, qce_kshard*
     return qce_set_error(QCE_EARG, "the shard model must hold components [" + std::to_string(lo) + ", " +
                                        std::to_string(hi) + ") of the balanced split (qce_kshard_slice)");
   DevGuard g(shard->device);
+  if (comm->kind == QCE_COMM_RCCL && comm->world > 1) shard->reserve_cus = kshard_reserve_cus();
   qce_kshard* ks = new qce_kshard();
   ks->m = shard;
   ks->mods[0] = shard;
@@ -912,6 +922,7 @@ int qce_kshard_set_spare(qce_kshard* ks, qce_model* spare) {
     KS_HIP(hipEventCreateWithFlags(&ks->ev_used[i], hipEventDisableTiming));
   }
   ks->mods[1] = spare;
+  spare->reserve_cus = ks->mods[0]->reserve_cus;
   return QCE_OK;
 }
 

@@ -79,6 +79,8 @@ struct qce_model {
   DevBuf<double2> WT;       // transposed filters W_k^T for the FP64 selective-mode kernel (built lazily)
   int wt_valid = 0;
   int cu_count = 256;
+  int reserve_cus = 0;  // QCE_OPT_RESERVE_CUS: CUs the persistent grids leave to a concurrent communication stream
+  int sched_cus() const { return cu_count - reserve_cus > 8 ? cu_count - reserve_cus : 8; }
   // dimensions beyond the fused kernels' 256 (qce_big.hip): GEMM-based FP64 path
   int big = 0;
   DevBuf<double2> big_ws, big_d;  // stacked transposed filters (N x K x M); per-chunk intermediate

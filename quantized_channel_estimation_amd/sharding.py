@@ -121,12 +121,12 @@ def _packed_to_complex(rows):
 
 
 def default_chunks(world):
-    """Pipeline chunks per batch: 2 at every rank count.  Measured per rank on one MI355X at the metric config
-    (tools/kshard_rank_sim.py, profiles/r03_kshard_rank_sim.txt): prepare + 1/2/4/8 partial launches take
-    1.49/1.51/1.66/1.92 ms at K/N = 16 (8 ranks), 2.62/2.68/2.84/3.10 at 32 and 4.99/5.07/5.18/5.46 at 64 -- every
-    extra chunk adds stream-K tails and merges -- while only the last chunk's reduce-scatter (1/c of ~0.3-0.5 ms)
-    is exposed, so two chunks give the smallest sum at N = 2, 4 and 8."""
-    return 2
+    """Pipeline chunks per batch: 1.  Per rank on one MI355X through qce_kshard_* (profiles/r05_kshard_rank16.jsonl,
+    r05_kshard_rank_cfg4.jsonl): 1.22 / 1.34 ms per step with 1 / 2 chunks at the metric's K = 16 per rank, 5.36 /
+    5.60 ms at cfg4's K = 32 -- a second chunk adds a launch tail and a merge to every step.  With the library's
+    send rows alternating between two buffers, step t's reduce-scatter already runs beside step t+1's kernel (on the
+    CUs the shard's grid leaves free, QCE_OPT_RESERVE_CUS), so a chunk split buys no overlap in a run of steps."""
+    return 1
 
 
 class ComponentShardEstimator:

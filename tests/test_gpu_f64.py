@@ -263,3 +263,21 @@ def test_f64_3m_matches_4m_and_oracle(N, M_pilots, mean, monkeypatch):
     tol = F64_TOL if M_pilots == 1 else 1e-6  # 1 bit with a general A: the arcsine law's documented sensitivity
     assert rel_fro(h3, ho) < tol, rel_fro(h3, ho)
     dm.close()
+
+
+def test_reserved_cus_same_estimate():
+    """QCE_OPT_RESERVE_CUS (set by the K-shard step at world > 1 so the reduce-scatter kernels find free CUs): the
+    persistent grid shrinks, the estimate is the same FP64 computation (1e-12; the stream-K split differs)."""
+    _gpu_or_skip()
+    from quantized_channel_estimation_amd import _lib
+    means, covs, w, h, y, qz = _synthetic(128, 64, 9000, 77, 1)
+    dm = _lib.DeviceModel(means, covs, w)
+    dm.prepare(None, 5.0, 1.0)
+    h0 = dm.estimate(y)
+    m0, s0, a0 = dm.partial64(y)
+    for n in (16, 40, 250):
+        dm.reserve_cus(n)
+        assert rel_fro(dm.estimate(y), h0) < 1e-12
+        m1, s1, a1 = dm.partial64(y)
+        assert rel_fro(a1 * np.exp(m1 - m0)[:, None], a0) < 1e-12
+    dm.close()

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--kind", default="rccl", choices=["rccl", "host"])
     ap.add_argument("--single-buffer", action="store_true", help="no spare table set (prepare not overlapped)")
+    ap.add_argument("--reserve", type=int, default=0,
+                    help="CUs the shard's grid leaves free (QCE_OPT_RESERVE_CUS; the library sets 16 at world > 1)")
     a = ap.parse_args()
     import torch
     from quantized_channel_estimation_amd import inputs
@@ -41,6 +43,10 @@ def main():
         dist.init_process_group("gloo", rank=0, world_size=1)
     comm = make_comm(0, 1, 0, kind=a.kind)
     est = ComponentShardEstimator(means, covs, w, 0, 1, device=0, comm=comm, double_buffer=not a.single_buffer)
+    if a.reserve:
+        est.dev.reserve_cus(a.reserve)
+        if getattr(est.native, "spare", None) is not None:
+            est.native.spare.reserve_cus(a.reserve)
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     yd = torch.from_numpy(y).cuda()
@@ -62,7 +68,7 @@ def main():
     r = rows.cpu().numpy()[:512]
     ho = O.estimate(means, covs, w, y[r], 5.0, a.N, None, "all", 1)
     err = float(np.linalg.norm(hk[:512].cpu().numpy() - ho) / np.linalg.norm(ho))
-    print(json.dumps(dict(kind=a.kind, double_buffer=not a.single_buffer, K=a.K, N=a.N, B=a.B, chunks=a.chunks, steps=a.steps, ms_per_step=dt * 1e3,
+    print(json.dumps(dict(kind=a.kind, double_buffer=not a.single_buffer, K=a.K, N=a.N, B=a.B, chunks=a.chunks, reserve_cus=a.reserve, steps=a.steps, ms_per_step=dt * 1e3,
                           partial_kernel_ms_per_step=kms / a.steps, launches=nl, est_per_s=a.B / dt,
                           parity_rel_fro=err)), flush=True)
 
