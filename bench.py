@@ -86,6 +86,10 @@ def parse():
     ap.add_argument("--dropin", action="store_true",
                     help="add the drop-in (numpy host I/O) side line; off by default because its chunked launches of "
                          "the headline kernel would enter a rocprof kernel-stats average of the bench command")
+    ap.add_argument("--sweep", action="store_true",
+                    help="one GPU: the reference's SNR loop (Bussgang_GMM.py:43, :284-287: snrs -10..20 dB, one batch "
+                         "of B observations per point) with double-buffered per-SNR tables (sweep.SnrSweep: the prepare "
+                         "of point t+1 beside the estimate of point t), against the same loop prepare-then-estimate")
     ap.add_argument("--launch-check", action="store_true",
                     help="CPU rehearsal of the launcher: ranks rendezvous over gloo, barrier + MAX-over-ranks "
                          "timing, rank 0 prints one JSON line; no GPU is touched")
@@ -450,6 +454,79 @@ def dropin_line(cfg, means, covs, w, y, quantizer, calls=3):
                 io="host numpy complex128 in/out, state mirror lazy")
 
 
+# ------------------------------------------------------------------------------------------ SNR sweep
+SWEEP_SNRS = [-10, -5, 0, 5, 10, 15, 20]  # Bussgang_GMM.py:43
+
+
+def sweep_main(args):
+    """--sweep: the reference's SNR loop on one GPU, one batch per SNR point, prepare + estimate per point; the
+    double-buffered SnrSweep against the serial loop on one model.  One JSON line."""
+    import torch
+    from quantized_channel_estimation_amd import _lib
+    from quantized_channel_estimation_amd.sweep import SnrSweep
+    cfg = dict(CONFIGS[args.config])
+    if cfg.pop("dense", False):
+        os.environ["QCE_FFT"] = "0"
+    if args.batch:
+        cfg["B"] = args.batch
+    K, N, B = cfg["K"], cfg["N"], cfg["B"]
+    qkind = {"uniform": _lib.QUANT_UNIFORM, "lloyd": _lib.QUANT_LLOYD}[cfg["qtype"]]
+    points_host = []
+    for i, snr in enumerate(SWEEP_SNRS):
+        c = dict(cfg, snr=float(snr))
+        means, covs, w, h, y, qz = make_inputs(c, i)
+        thr, lab = (qz[0], qz[1]) if c["n_bits"] not in (1, np.inf) and c["qtype"] == "lloyd" else (None, None)
+        points_host.append((float(snr), y, h, qz, thr, lab))
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    pts = [(None, snr, cfg["n_bits"], qkind, thr, lab, torch.from_numpy(y).to(dev))
+           for snr, y, h, qz, thr, lab in points_host]
+    outs = [torch.empty((B, N), dtype=torch.complex128, device=dev) for _ in pts]
+    sw = SnrSweep(means, covs, w, reserve_cus=int(os.environ.get("QCE_SWEEP_RESERVE", "32")))
+    single = _lib.DeviceModel(means, covs, w)
+    sptr = stream.cuda_stream
+
+    def serial():
+        for (A, snr, nb, qk, thr, lab, y), o in zip(pts, outs):
+            single.prepare(A, snr, nb, qk, thr, lab, stream=sptr)
+            single.estimate(y, _lib.MODE_ALL, 0.0, out=o, stream=sptr)
+
+    def timed(fn):
+        for _ in range(max(1, args.warmup)):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / (args.steps * len(pts))
+
+    t_ser = timed(serial)
+    ref = [o.cpu().numpy() for o in outs]
+    t_dbl = timed(lambda: sw.run(pts, outs=outs, stream=stream))
+    got = [o.cpu().numpy() for o in outs]
+    dev_vs_serial = max(float(np.linalg.norm(g - r) / np.linalg.norm(r)) for g, r in zip(got, ref))
+    parity = None
+    if not args.no_parity:
+        from oracle import qce_oracle as O
+        snr, y, h, qz, thr, lab = points_host[3]
+        ho = O.estimate(means, covs, w, y[:512], snr, N, None, "all", cfg["n_bits"], cfg["qtype"], qz)
+        parity = dict(snr=snr, samples=512, rel_fro=float(np.linalg.norm(got[3][:512] - ho) / np.linalg.norm(ho)))
+    line = {"metric": METRIC + " (SNR sweep)", "value": round(B / t_dbl, 1), "unit": "channel estimates/s",
+            "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_snr_point": round(t_dbl * 1e3, 4),
+            "ms_per_snr_point_serial": round(t_ser * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic: one seeded batch per SNR point",
+            "config": {"workload": f"SNR sweep {SWEEP_SNRS} dB, per point estimate_from_y K={K} N=M={N} "
+                                   f"cov={cfg['cov']} n_bits={cfg['n_bits']} {cfg['qtype']} mode=all B={B}",
+                       "K": K, "N": N, "B": B, "points": len(pts), "tables": "double-buffered (sweep.SnrSweep)"},
+            "kernel": single.kernel(), "max_rel_dev_vs_serial": dev_vs_serial, "parity": parity}
+    print(json.dumps(line), flush=True)
+    sw.close()
+    single.close()
+    return 0
+
+
 # ------------------------------------------------------------------------------------------ main
 def main():
     args = parse()
@@ -457,6 +534,10 @@ def main():
         sys.exit(launch_ranks(args.gpus))
     if args.launch_check:
         return launch_check(args)
+    if args.sweep:
+        if args.gpus != 1:
+            raise SystemExit("bench.py --sweep runs on one GPU")
+        return sweep_main(args)
     cfg = dict(CONFIGS[args.config])
     if cfg.pop("dense", False):
         os.environ["QCE_FFT"] = "0"  # read by qce_prepare: keep the structured mixture on the dense path

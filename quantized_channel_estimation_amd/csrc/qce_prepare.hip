@@ -394,28 +394,32 @@ __global__ __launch_bounds__(256) void k_chol_inv(int M, double2* __restrict__ L
 //   inverse :  X~_ic -= a_ij / a_jj * X~_jc      (i > j, c <= j; row j of X~ is final)
 //              afterwards Linv_ic = X~_ic / sqrt(a_ii)
 // (reads and writes of a step touch disjoint entries, so no second barrier is needed; M barriers in all).
-__global__ __launch_bounds__(256) void k_chol_inv_lds(int M, const double2* __restrict__ Cr,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_chol_inv_lds(int M, const double2* __restrict__ Cr,
                                                       double2* __restrict__ Linv, const double* __restrict__ logw,
                                                       double* __restrict__ cconst, int* __restrict__ status) {
-  __shared__ double2 a[64 * 64];
-  __shared__ double2 x[64 * 64];
+  // row stride 65: the steps read columns (a_rj, a_cj, a_ij for many r at one j); with a 1 KB stride every such
+  // read of a wave hit one LDS bank group
+  constexpr int LD = 65;
+  __shared__ double2 a[64 * LD];
+  __shared__ double2 x[64 * LD];
   __shared__ double piv[64];
   // (row, column) of the row-major lower triangle of the trailing block per entry t: every step's triangle is a
   // prefix of the largest one, so one table serves all steps (no per-entry square root)
   __shared__ unsigned short tri_rc[63 * 64 / 2];
   const int k = blockIdx.x, tid = threadIdx.x;
   const double2* src = Cr + (long long)k * M * M;
-  for (int e = tid; e < M * M; e += 256) {
+  for (int e = tid; e < M * M; e += NT) {
     const int r = e / M, c = e % M;
-    a[r * 64 + c] = src[e];
-    x[r * 64 + c] = make_double2(r == c ? 1.0 : 0.0, 0.0);
+    a[r * LD + c] = src[e];
+    x[r * LD + c] = make_double2(r == c ? 1.0 : 0.0, 0.0);
   }
-  for (int rr = tid >> 6; rr < 63; rr += 4)
+  for (int rr = tid >> 6; rr < 63; rr += NT / 64)
     for (int cc = tid & 63; cc <= rr; cc += 64) tri_rc[rr * (rr + 1) / 2 + cc] = (unsigned short)((rr << 8) | cc);
   __syncthreads();
   bool bad = false;
   for (int j = 0; j < M; ++j) {
-    const double ajj = a[j * 64 + j].x;  // final: updated by step j - 1 before the barrier
+    const double ajj = a[j * LD + j].x;  // final: updated by step j - 1 before the barrier
     if (!(ajj > 0.0)) {                  // same value in every thread: uniform exit
       bad = true;
       break;
@@ -423,24 +427,24 @@ __global__ __launch_bounds__(256) void k_chol_inv_lds(int M, const double2* __re
     const double inv = 1.0 / ajj;
     const int n = M - j - 1;
     const int tri = n * (n + 1) / 2;
-    for (int t = tid; t < tri; t += 256) {
+    for (int t = tid; t < tri; t += NT) {
       const unsigned v = tri_rc[t];  // t -> (r, c), r >= c, in the trailing block
       const int r = j + 1 + (int)(v >> 8), c = j + 1 + (int)(v & 255u);
-      const double2 arj = a[r * 64 + j], acj = a[c * 64 + j];
+      const double2 arj = a[r * LD + j], acj = a[c * LD + j];
       const double2 pr = cmulc(arj, acj);
-      a[r * 64 + c] = csub(a[r * 64 + c], make_double2(pr.x * inv, pr.y * inv));
+      a[r * LD + c] = csub(a[r * LD + c], make_double2(pr.x * inv, pr.y * inv));
     }
     // inverse step j in the same phase: it needs column j of the factor (final since step j - 1, not written by
     // the update above) and row j of X~ (final since step j - 1), and writes only X~ rows below j
     const int nr = M - j - 1, nc = j + 1;
     const float rnc = 1.0f / (float)nc;  // t / nc through an fp32 reciprocal and one correction (t < 4096)
-    for (int t = tid; t < nr * nc; t += 256) {
+    for (int t = tid; t < nr * nc; t += NT) {
       int q = (int)((float)t * rnc);
       q += (q + 1) * nc <= t ? 1 : 0;
       q -= q * nc > t ? 1 : 0;
       const int i = j + 1 + q, c = t - q * nc;
-      const double2 l = a[i * 64 + j];
-      x[i * 64 + c] = csub(x[i * 64 + c], cmul(make_double2(l.x * inv, l.y * inv), x[j * 64 + c]));
+      const double2 l = a[i * LD + j];
+      x[i * LD + c] = csub(x[i * LD + c], cmul(make_double2(l.x * inv, l.y * inv), x[j * LD + c]));
     }
     __syncthreads();
   }
@@ -448,12 +452,12 @@ __global__ __launch_bounds__(256) void k_chol_inv_lds(int M, const double2* __re
     if (tid == 0) status[k] = 1;
     return;
   }
-  for (int i = tid; i < M; i += 256) piv[i] = sqrt(a[i * 64 + i].x);
+  for (int i = tid; i < M; i += NT) piv[i] = sqrt(a[i * LD + i].x);
   __syncthreads();
   double2* dst = Linv + (long long)k * M * M;
-  for (int e = tid; e < M * M; e += 256) {
+  for (int e = tid; e < M * M; e += NT) {
     const int r = e / M, c = e % M;
-    const double2 v = x[r * 64 + c];
+    const double2 v = x[r * LD + c];
     dst[e] = make_double2(v.x / piv[r], v.y / piv[r]);
   }
   if (tid == 0) {
@@ -791,7 +795,20 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
     return 1;
   }();
   if (M <= 64 && chol64 == 1) {
-    hipLaunchKernelGGL(k_chol_inv_lds, dim3(K), dim3(256), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
+    // threads per component (QCE_CHOL_THREADS, A/B): the early steps' trailing triangles (up to 2016 entries) spread
+    // over more lanes; the late steps are latency-bound either way.  Whole prepare, metric / cfg2
+    // (profiles/r05_prepare_chol_threads.jsonl): 256 threads 0.184 / 0.170 ms, 512 0.164 / 0.153, 1024 0.160 / 0.146
+    static const int nt = [] {
+      const char* e = getenv("QCE_CHOL_THREADS");
+      const int v = e ? atoi(e) : 1024;
+      return (v == 256 || v == 512 || v == 1024) ? v : 1024;
+    }();
+    if (nt == 1024)
+      hipLaunchKernelGGL(k_chol_inv_lds<1024>, dim3(K), dim3(1024), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
+    else if (nt == 512)
+      hipLaunchKernelGGL(k_chol_inv_lds<512>, dim3(K), dim3(512), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
+    else
+      hipLaunchKernelGGL(k_chol_inv_lds<256>, dim3(K), dim3(256), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
   } else if (M <= 64 && chol64 == 2) {
     hipLaunchKernelGGL(k_chol_inv_tri<64>, dim3(K), dim3(256), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
   } else if (M <= 64) {

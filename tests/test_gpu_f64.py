@@ -281,3 +281,29 @@ def test_reserved_cus_same_estimate():
         m1, s1, a1 = dm.partial64(y)
         assert rel_fro(a1 * np.exp(m1 - m0)[:, None], a0) < 1e-12
     dm.close()
+
+
+def test_snr_sweep_double_buffered_matches_serial():
+    """sweep.SnrSweep (two table sets; the prepare of SNR point t+1 on its own stream beside the estimate of point t,
+    Bussgang_GMM.py:284-287): every point equals the single-model prepare-then-estimate result (1e-12), over the
+    reference's SNR list with one batch per point, 1 bit and 2-bit uniform."""
+    _gpu_or_skip()
+    import torch
+    from quantized_channel_estimation_amd import _lib
+    from quantized_channel_estimation_amd.sweep import SnrSweep
+    for nb in (1, 2):
+        means, covs, w, _, _, _ = _synthetic(32, 64, 10, 91, nb)
+        pts, ys = [], []
+        for i, snr in enumerate([-10, -5, 0, 5, 10, 15, 20]):
+            _, _, _, _, y, _ = _synthetic(32, 64, 3000, 91 + i, nb, snr=float(snr))
+            ys.append(y)
+            pts.append((None, float(snr), nb, _lib.QUANT_UNIFORM, None, None, torch.from_numpy(y).cuda()))
+        sw = SnrSweep(means, covs, w)
+        outs = sw.run(pts)
+        torch.cuda.synchronize()
+        single = _lib.DeviceModel(means, covs, w)
+        for (A, snr, _, _, _, _, _), y, h in zip(pts, ys, outs):
+            single.prepare(None, snr, nb)
+            assert rel_fro(h.cpu().numpy(), single.estimate(y)) < 1e-12, (nb, snr)
+        sw.close()
+        single.close()
