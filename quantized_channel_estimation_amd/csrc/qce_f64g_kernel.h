@@ -51,6 +51,11 @@
 #ifndef QCE_F64G_CB
 #define QCE_F64G_CB 0
 #endif
+// waves 4-7 (the second wave of every SIMD) consume the ring LAG chunks behind waves 0-3, so the two waves of a SIMD
+// reach their softmax and GL folds at different times (the ring keeps LAG more chunks; 0 = lockstep)
+#ifndef QCE_F64G_LAG
+#define QCE_F64G_LAG 0
+#endif
 // 1: libm exp for the softmax weights (A/B builds)
 #ifndef QCE_F64G_LIBM_EXP
 #define QCE_F64G_LIBM_EXP 0
@@ -105,6 +110,7 @@ struct F64G3 {
   static constexpr int NWG = QCE_F64G_NW;  // waves per workgroup
   static constexpr int LDS_KB = NWG == 8 ? 144 : 72;
   static constexpr int CB = f64g_cb(BLOCKS);
+  static constexpr int LAG = QCE_F64G_LAG;
   static constexpr int NSLOT = LDS_KB / CB < 8 ? LDS_KB / CB : 8;
   static constexpr int CHUNK = CB * 1024;
   static constexpr int BPC = f64g_bpc(BLOCKS);
@@ -155,7 +161,8 @@ __global__ __launch_bounds__(QCE_F64G_NW * 64) __attribute__((amdgpu_waves_per_e
   constexpr double RESCALE = 32.0;  // lazy max: rescale only when lp exceeds m by this
   static_assert(G::CB % NW == 0, "chunk split");
   static_assert(E < G::CB, "the prefetch window must stay inside one chunk");
-  static_assert(G::NSLOT >= 3, "ring depth");
+  static_assert(G::NSLOT >= 3 + G::LAG, "ring depth");
+  static_assert(G::LAG == 0 || NW == 8, "lag: two waves per SIMD in one workgroup");
   __shared__ __attribute__((aligned(16))) char lds[G::NSLOT * G::CHUNK];
   __shared__ double etab[32];  // 2^(j/32) for exp_tab64
 
@@ -190,20 +197,31 @@ __global__ __launch_bounds__(QCE_F64G_NW * 64) __attribute__((amdgpu_waves_per_e
   auto refill_pieces = [&](int lo, int hi) {
     for (int i = lo; i < hi; ++i) lds_dma16(rsrc + i * NW * 1024, lds + rdst + i * NW * 1024);
   };
+  // chunk k lands by barrier k: at barrier k the slot of chunk k - LAG - 2 is free (the lagging waves are done
+  // with it) and takes chunk k + NSLOT - LAG - 2
   auto boundary_wait = [&]() {
-    wait_vmcnt<(G::NSLOT - 3) * LPW>();
+    wait_vmcnt<(G::NSLOT - 3 - G::LAG) * LPW>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     F64_STAMP(3);
   };
 #pragma unroll 1
-  for (int j = 0; j < G::NSLOT - 2; ++j) {
+  for (int j = 0; j < G::NSLOT - 2 - G::LAG; ++j) {
     refill_begin();
     refill_pieces(0, LPW);
   }
   boundary_wait();  // chunk 0
   refill_begin();
   refill_pieces(0, LPW);
+  const bool lagging = G::LAG > 0 && wave >= NW / 2;  // wave-uniform
+  if (lagging) {  // the lagging waves' first LAG barriers: refills only
+#pragma unroll 1
+    for (int j = 0; j < G::LAG; ++j) {
+      boundary_wait();
+      refill_begin();
+      refill_pieces(0, LPW);
+    }
+  }
   int cstream = 0;
 
   for (long long seg = 0; seg < nseg; ++seg) {
@@ -450,6 +468,14 @@ __global__ __launch_bounds__(QCE_F64G_NW * 64) __attribute__((amdgpu_waves_per_e
             }
         }
       }
+    }
+  }
+  if (G::LAG > 0 && !lagging) {  // the leading waves' last LAG barriers, matching the lagging waves' first ones
+#pragma unroll 1
+    for (int j = 0; j < G::LAG; ++j) {
+      boundary_wait();
+      refill_begin();
+      refill_pieces(0, LPW);
     }
   }
   F64_STAMP(5);
