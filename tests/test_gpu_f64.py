@@ -307,3 +307,20 @@ def test_snr_sweep_double_buffered_matches_serial():
             assert rel_fro(h.cpu().numpy(), single.estimate(y)) < 1e-12, (nb, snr)
         sw.close()
         single.close()
+
+
+def test_bench_sweep_line():
+    """bench.py --sweep (the reference's SNR list, one batch per point, double-buffered tables) prints one JSON line
+    whose points equal the serial loop and match the FP64 oracle."""
+    _gpu_or_skip()
+    import json
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--config", "cfg1", "--sweep", "--steps", "3",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert r["config"]["points"] == 7 and r["max_rel_dev_vs_serial"] < 1e-12
+    assert r["parity"]["rel_fro"] < 1e-9 and r["ms_per_snr_point"] > 0
