@@ -727,8 +727,8 @@ def main():
     if rank == 0 and world == 1 and not args.no_extras and args.config == "metric":
         extras["fast_path"] = fast_line(cfg, means, covs, w, yd, out, stream, max(3, args.steps // 2), qargs, ho,
                                         n_chk)
-        if args.dropin:
-            extras["dropin"] = dropin_line(cfg, means, covs, w, y, quantizer)
+    if rank == 0 and world == 1 and args.dropin:
+        extras["dropin"] = dropin_line(cfg, means, covs, w, y, quantizer)
     if rank == 0:
         line = {
             "metric": METRIC,
