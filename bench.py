@@ -86,6 +86,9 @@ def parse():
     ap.add_argument("--dropin", action="store_true",
                     help="add the drop-in (numpy host I/O) side line; off by default because its chunked launches of "
                          "the headline kernel would enter a rocprof kernel-stats average of the bench command")
+    ap.add_argument("--mean", action="store_true",
+                    help="components with non-zero means (0.3 x CN(0, 1) per entry, seeded): the reference's fit "
+                         "default zero_mean=False (gmm_cplx_bussgang.py:96-100); the bench configs are zero-mean")
     ap.add_argument("--sweep", action="store_true",
                     help="one GPU: the reference's SNR loop (Bussgang_GMM.py:43, :284-287: snrs -10..20 dB, one batch "
                          "of B observations per point) with double-buffered per-SNR tables (sweep.SnrSweep: the prepare "
@@ -171,6 +174,8 @@ def make_inputs(cfg, seed, pool=2048):
     from quantized_channel_estimation_amd import inputs
     K, N, B = cfg["K"], cfg["N"], cfg["B"]
     means, covs, w = inputs.synthetic_model(K, N, cov_type=cfg["cov"], blocks=cfg.get("blocks"))
+    if cfg.get("mean"):
+        means = 0.3 * inputs.crandn(K, N, rng=np.random.default_rng(12))
     rng = np.random.default_rng(1000 + seed)
     hp, _ = inputs.scm_generate(min(pool, B), 1, N, rng, n_path=3)
     hp = hp[:, 0, :].astype(np.complex128)
@@ -330,7 +335,8 @@ def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
         bytes_per_launch = 32.0 * N * B
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
         n1, n2, _ = dm.structure()
-        fft_flops = (4.0 * k_local * N + 10.0 * N * math.log2(N)) * B  # D3: zero-mean FFT-path flops
+        # D3: 4 K N MFMA flops per estimate (zero mean; 12 K N with means: + 2 Re(Y^* u) in lp, + b in the filter)
+        fft_flops = ((12.0 if dm_has_mean(dm) else 4.0) * k_local * N + 10.0 * N * math.log2(N)) * B
         return dict(bound="hbm", achieved=round(achieved, 2), peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=round(achieved / HBM_PEAK_GBS, 4), traffic=traffic,
                     kernel=fourier_kernel(N, dm_has_mean(dm)),
@@ -339,7 +345,8 @@ def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
                     fp64_flops_per_launch=fft_flops, fp64_tflops=round(fft_flops / (kern_ms * 1e-3) / 1e12, 3),
                     fp64_frac=round(fft_flops / (kern_ms * 1e-3) / 1e12 / FP64_MFMA_PEAK_TFLOPS, 4),
                     note="HBM roofline per SURVEY D3 (32 N B per estimate); the kernel's binding resource is FP64 "
-                         "issue (4 K N MFMA + FFT VALU flops per estimate), reported as fp64_frac")
+                         "issue (4 K N MFMA flops per estimate, 12 K N with means, + FFT VALU flops), reported as "
+                         "fp64_frac")
     M = N  # A = I at every bench config (n_pilots = 1)
     flops = 16.0 * k_local * N * N * B  # 16 K M N real flops per estimate (dense count)
     if dm.precision == "f64":
@@ -391,12 +398,14 @@ def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
 
 def fourier_kernel(N, has_mean):
     """The Fourier-path kernel qce_fft_mfma.hip runs for this shape (QCE_FFT_CHUNK=0 selects the round-2 kernels)."""
-    new = os.environ.get("QCE_FFT_CHUNK", "1") != "0" and not has_mean
-    if N == 64 and new:
+    new = os.environ.get("QCE_FFT_CHUNK", "1") != "0"
+    if N == 64 and new and not has_mean:
         return "k_fft_wreg"
     if N <= 64:
         return "k_fft_wave"
-    return "k_fft_chunk" if new else "k_fft_mfma"
+    if not new:
+        return "k_fft_mfma"
+    return "k_fft_chunk_hm" if has_mean else "k_fft_chunk"
 
 
 def dtype_of(dm):
@@ -558,6 +567,8 @@ def main():
         cfg["B"] = args.batch
     if args.components:
         cfg["K"] = args.components
+    if args.mean:
+        cfg["mean"] = True
     K, N, B = cfg["K"], cfg["N"], cfg["B"]
     data_seed = rank if args.shard == "batch" else 0
     means, covs, w, h, y, quantizer = make_inputs(cfg, data_seed)
@@ -745,7 +756,7 @@ def main():
             "dtype": dtype_of(dm),
             "data": f"synthetic: seeded {cfg['cov']} SCM-derived covariances, SCM channel pool + fresh CN noise, "
                     f"{cfg['n_bits']}-bit {cfg['qtype']} quantised",
-            "config": {"workload": f"estimate_from_y K={K} N=M={N} cov={cfg['cov']} n_bits={cfg['n_bits']} "
+            "config": {"workload": f"estimate_from_y K={K} N=M={N} cov={cfg['cov']}{' with means' if args.mean else ''} n_bits={cfg['n_bits']} "
                                    f"{cfg['qtype']} snr={cfg['snr']}dB mode=all B={B}"
                                    f"{'' if args.shard == 'k' else '/GPU'} prepare-per-step",
                        "K": K, "N": N, "B": B, "shard": args.shard,

@@ -10,8 +10,9 @@
 //   k_fft_wreg   zero-mean N = 64: persistent one-wave tiles, register transform (pass 1 / LDS exchange / pass 2)
 //   k_fft_chunk  zero-mean N = 128, 256: components split over the waves for lp / softmax, bins for the filter,
 //                two barriers per 128-component chunk; register transform for N = 256
+//   k_fft_chunk_hm  N = 128, 256 with means: k_fft_chunk's split, spectra kept in the LDS tile, 3x the MFMAs
 //   k_fft_wave   N = 16, 32 and models with means up to 64 (wave-local LDS transform)
-//   k_fft_mfma   N = 128, 256 with means (described next)
+//   k_fft_mfma   N = 128, 256 with QCE_FFT_CHUNK=0 (the round-2 kernel, described next)
 // On gfx950 FP64 VALU instructions and FP64 MFMAs share the SIMD's issue budget (tools/probe/f64_pipe_probe.hip),
 // so the newer kernels are organised around fewer VALU instructions per MFMA.
 //
@@ -1531,6 +1532,320 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
   FW_STAMP_FLUSH
 }
 
+// Models with means, N = 128, 256 (the reference's fit default zero_mean=False, gmm_cplx_bussgang.py:96-100; the
+// means enter at :256-264, :288): k_fft_chunk's split (components over the waves for lp / softmax, bins over the waves
+// for the filter, two barriers per chunk of 128 components) with the mean terms of the Fourier-domain formula
+//   lp_k = c'_k - sum_i |Y_i|^2 r_ik + 2 sum_i (Re Y_i Re u_ik + Im Y_i Im u_ik)    (u_ik = (mu_y)_ik / r_ik)
+//   Z_i  = Y_i f_i + sum_k gamma_k b_ik                                            (f_i = sum_k gamma_k w_ik)
+// i.e. two more real MFMAs per lp k-step (B = Re Y, Im Y read from the spectra tile) and two more filter accumulator
+// sets (Re b, Im b): 3x the zero-mean MFMA work.  The spectra stay in the LDS tile through the component loop (Z is
+// formed from it at the end), so |Y|^2, e and the column statistics get their own LDS (118 KB at N = 256: one
+// workgroup per CU, one wave per SIMD with up to 512 registers, the accumulators in AGPRs).  Tables in k_fft_chunk's
+// fragment order (k_fft_pack with frag, pur / pui beside pr, pbr / pbi beside pw).
+template <int N>
+struct FftChunkHmLds {
+  static constexpr int TS = 16, RS = N + 1;
+  static constexpr size_t tile = (size_t)TS * RS * 16;
+  static constexpr size_t y2 = (size_t)N * TS * 8, e = (size_t)128 * TS * 8, sm = (size_t)2 * 4 * TS * 8;
+  static constexpr size_t bytes = 128 * 16 + tile + y2 + e + sm + 32 * 8;
+};
+
+template <int N, int OUT>
+__global__ __launch_bounds__(256, 1) void k_fft_chunk_hm(long long B, int lg1, int lg2, int Kp,
+                                                         const double2* __restrict__ y, const double* __restrict__ pr,
+                                                         const double* __restrict__ pur, const double* __restrict__ pui,
+                                                         const double* __restrict__ pc, const double* __restrict__ pw,
+                                                         const double* __restrict__ pbr,
+                                                         const double* __restrict__ pbi, double2* __restrict__ h,
+                                                         double* __restrict__ om, double* __restrict__ os,
+                                                         float* __restrict__ oa) {
+  using LD = FftChunkHmLds<N>;
+  constexpr int TS = 16, RS = N + 1, lgTS = 4;
+  constexpr int lgN = __builtin_ctz(N);
+  constexpr int NB = N / 4, NTW = NB / 16, NTF = N / 16, NL = N / 8, NWF = N / 8, CB = 8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  double2* tw = reinterpret_cast<double2*>(smem);
+  double2* T = tw + 128;                                                         // spectra, kept through the loop
+  double2* Y2 = reinterpret_cast<double2*>(reinterpret_cast<char*>(T) + LD::tile);  // [N/8][4][16]
+  double2* E = reinterpret_cast<double2*>(reinterpret_cast<char*>(Y2) + LD::y2);    // [CB * 2][4][16]
+  double* SM = reinterpret_cast<double*>(reinterpret_cast<char*>(E) + LD::e);       // [2][4][16]
+  double* etab = reinterpret_cast<double*>(reinterpret_cast<char*>(SM) + LD::sm);  // 2^(j/32)
+  const int tid = threadIdx.x;
+  const long long b0 = (long long)blockIdx.x * TS;
+  const int rows = (int)((B - b0) < TS ? (B - b0) : TS);
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int col = lane & 15, hq = lane >> 4;
+  const int bin0 = wid * NB;
+  double2* Trow = T + col * RS;
+  // the lane's filter-phase storage position of tile t, accumulator row hq + 4 r
+  auto fpos = [&](int t, int r) -> int {
+    return N == 256 ? 16 * (hq + 4 * wid) + r + 4 * t : bin0 + 16 * t + hq + 4 * r;
+  };
+  if constexpr (N == 256) {
+    const int s1 = tid >> 4, g = tid & 15;
+    const double2* yr = y + (b0 + (s1 < rows ? s1 : rows - 1)) * N + g;
+    double2 x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = yr[16 * i];
+    for (int t = tid; t < 128; t += 256) {
+      double sn, cs;
+      sincospi(-(double)t / 128.0, &sn, &cs);
+      tw[t] = make_double2(cs, sn);
+    }
+    exp2_tab_init(etab, tid);
+    __syncthreads();
+    if (s1 >= rows) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) x[i] = make_double2(0.0, 0.0);
+    }
+    fft256_pass1<false>(x, lg2, g, tw);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) T[s1 * RS + g + 16 * i] = x[i];
+    __syncthreads();
+    double2 yv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) yv[i] = Trow[16 * (hq + 4 * wid) + i];
+    fft_pass_low4<false>(yv, lg2, tw);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Trow[16 * (hq + 4 * wid) + i] = yv[i];  // the lane's own points: no barrier needed
+#pragma unroll
+    for (int tp = 0; tp < 2; ++tp)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double2 a = yv[r + 8 * tp], b = yv[r + 8 * tp + 4];
+        Y2[((2 * (hq + 4 * wid) + tp) * 4 + r) * 16 + col] = make_double2(a.x * a.x + a.y * a.y, b.x * b.x + b.y * b.y);
+      }
+    __syncthreads();
+  } else {
+    for (int t = tid; t < 128; t += 256) {
+      double sn, cs;
+      sincospi(-(double)t / 128.0, &sn, &cs);
+      tw[t] = make_double2(cs, sn);
+    }
+    exp2_tab_init(etab, tid);
+    {
+      constexpr int NLY = TS * N / 256;
+      const double2* yt = y + b0 * N;
+      double2 v[NLY];
+#pragma unroll
+      for (int i = 0; i < NLY; ++i) {
+        const int e = tid + 256 * i, r = e >> lgN;
+        v[i] = yt[(r < rows ? r : rows - 1) * N + (e & (N - 1))];
+      }
+#pragma unroll
+      for (int i = 0; i < NLY; ++i) {
+        const int e = tid + 256 * i, r = e >> lgN;
+        T[r * RS + (e & (N - 1))] = (r < rows) ? v[i] : make_double2(0.0, 0.0);
+      }
+    }
+    __syncthreads();
+    fft_axis_passes<false>(T, lgTS, RS, lgN, lg2, 1, tw);
+    if (lg1 > 0) fft_axis_passes<false>(T, lgTS, RS, lgN, lg1, 1 << lg2, tw);
+    {
+      constexpr int NP = N * TS / 2 / 256;
+#pragma unroll
+      for (int j = 0; j < NP; ++j) {
+        const int p = tid + 256 * j, sI = p & 15, rest = p >> 4;
+        const int bq = 8 * (rest >> 2) + (rest & 3);
+        const double2 a = T[sI * RS + bq], b = T[sI * RS + bq + 4];
+        Y2[tid + 256 * j] = make_double2(a.x * a.x + a.y * a.y, b.x * b.x + b.y * b.y);
+      }
+    }
+    __syncthreads();
+  }
+
+  f64x4 F[NTW], Br[NTW], Bi[NTW];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t)
+    for (int r = 0; r < 4; ++r) F[t][r] = Br[t][r] = Bi[t][r] = 0.0;
+  double m = -__builtin_inf(), ssum = 0.0;
+  const int ncb = Kp >> 4;
+  const unsigned tb = (unsigned)(Kp * N * 8);
+  const __amdgpu_buffer_rsrc_t rpr = buf_rsrc(pr, tb), rpw = buf_rsrc(pw, tb);
+  const __amdgpu_buffer_rsrc_t rur = buf_rsrc(pur, tb), rui = buf_rsrc(pui, tb);
+  const __amdgpu_buffer_rsrc_t rbr = buf_rsrc(pbr, tb), rbi = buf_rsrc(pbi, tb);
+  const unsigned ul16 = (unsigned)lane * 16;
+  const double2* Y2l = Y2 + hq * 16 + col;
+  for (int c0 = 0; c0 < ncb; c0 += CB) {
+    const int cb0 = c0 + wid, cb1 = cb0 + 4;
+    const bool v0 = cb0 < ncb, v1 = cb1 < ncb;  // wave-uniform
+    f64x4 C0, C1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      C0[r] = v0 ? pc[16 * cb0 + hq + 4 * r] : -__builtin_inf();
+      C1[r] = v1 ? pc[16 * cb1 + hq + 4 * r] : -__builtin_inf();
+    }
+    // lp k-steps 2i, 2i + 1, row hq: storage positions 8 i + hq, 8 i + 4 + hq (the Y2 pair, k_fft_pack layouts 0 / 1)
+    if (v0) {
+      const unsigned o0 = (unsigned)cb0 * NL * 1024, o1 = (unsigned)(v1 ? cb1 : cb0) * NL * 1024;
+#pragma unroll 4
+      for (int i = 0; i < NL; ++i) {
+        const double2 a0 = buf_ld2(rpr, ul16, o0 + 1024 * i), a1 = buf_ld2(rpr, ul16, o1 + 1024 * i);
+        const double2 u0 = buf_ld2(rur, ul16, o0 + 1024 * i), u1 = buf_ld2(rur, ul16, o1 + 1024 * i);
+        const double2 q0 = buf_ld2(rui, ul16, o0 + 1024 * i), q1 = buf_ld2(rui, ul16, o1 + 1024 * i);
+        const double2 b = Y2l[i * 64];
+        const double2 ya = Trow[8 * i + hq], yb = Trow[8 * i + 4 + hq];
+        C0 = mfma16x16x4d(a0.x, b.x, C0);
+        C1 = mfma16x16x4d(a1.x, b.x, C1);
+        C0 = mfma16x16x4d(a0.y, b.y, C0);
+        C1 = mfma16x16x4d(a1.y, b.y, C1);
+        C0 = mfma16x16x4d(u0.x, ya.x, C0);
+        C1 = mfma16x16x4d(u1.x, ya.x, C1);
+        C0 = mfma16x16x4d(q0.x, ya.y, C0);
+        C1 = mfma16x16x4d(q1.x, ya.y, C1);
+        C0 = mfma16x16x4d(u0.y, yb.x, C0);
+        C1 = mfma16x16x4d(u1.y, yb.x, C1);
+        C0 = mfma16x16x4d(q0.y, yb.y, C0);
+        C1 = mfma16x16x4d(q1.y, yb.y, C1);
+      }
+      if (!v1) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) C1[r] = -__builtin_inf();
+      }
+    }
+    const double lm = col_max4(fmax(fmax(fmax(C0[0], C0[1]), fmax(C0[2], C0[3])),
+                                    fmax(fmax(C1[0], C1[1]), fmax(C1[2], C1[3]))));
+    if (hq == 0) SM[wid * 16 + col] = lm;
+    __syncthreads();
+    const double mn = fmax(fmax(m, fmax(SM[col], SM[16 + col])), fmax(SM[32 + col], SM[48 + col]));
+    const double sh = (mn == -__builtin_inf()) ? 0.0 : mn;
+    const double alpha = exp_nonpos(m - sh, etab);
+    double ls = 0.0;
+    {
+      double e[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) e[r] = v0 ? exp_nonpos(C0[r] - sh, etab) : 0.0;
+      ls += (e[0] + e[1]) + (e[2] + e[3]);
+      E[((2 * wid) * 4 + hq) * 16 + col] = make_double2(e[0], e[1]);
+      E[((2 * wid + 1) * 4 + hq) * 16 + col] = make_double2(e[2], e[3]);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) e[r] = v1 ? exp_nonpos(C1[r] - sh, etab) : 0.0;
+      ls += (e[0] + e[1]) + (e[2] + e[3]);
+      E[((2 * (wid + 4)) * 4 + hq) * 16 + col] = make_double2(e[0], e[1]);
+      E[((2 * (wid + 4) + 1) * 4 + hq) * 16 + col] = make_double2(e[2], e[3]);
+    }
+    ls = col_sum4(ls);
+    if (hq == 0) SM[64 + wid * 16 + col] = ls;
+    __syncthreads();
+    ssum = ssum * alpha + ((SM[64 + col] + SM[80 + col]) + (SM[96 + col] + SM[112 + col]));
+    m = mn;
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) {
+      F[t] *= alpha;
+      Br[t] *= alpha;
+      Bi[t] *= alpha;
+    }
+    const int nbl = (ncb - c0) < CB ? (ncb - c0) : CB;
+    constexpr int NWL = 2 * NTW;
+    const unsigned wbase = (unsigned)c0 * NWF * 1024 + (unsigned)((wid * NTW) >> 1) * 1024;
+#pragma unroll 1
+    for (int bl = 0; bl < nbl; ++bl) {
+      const unsigned ob = wbase + (unsigned)bl * NWF * 1024;
+      double2 ww[NWL], wr[NWL], wi[NWL];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int tp = 0; tp < NTW / 2; ++tp) {
+          const unsigned o = ob + ((r * NTF) >> 1) * 1024 + tp * 1024;
+          ww[r * (NTW / 2) + tp] = buf_ld2(rpw, ul16, o);
+          wr[r * (NTW / 2) + tp] = buf_ld2(rbr, ul16, o);
+          wi[r * (NTW / 2) + tp] = buf_ld2(rbi, ul16, o);
+        }
+#pragma unroll
+      for (int rp = 0; rp < 2; ++rp) {
+        const double2 ev = E[((2 * bl + rp) * 4 + hq) * 16 + col];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+          const int r = 2 * rp + rr;
+          const double eb = rr ? ev.y : ev.x;
+#pragma unroll
+          for (int tp = 0; tp < NTW / 2; ++tp) {
+            const int j = r * (NTW / 2) + tp;
+            F[2 * tp] = mfma16x16x4d(ww[j].x, eb, F[2 * tp]);
+            F[2 * tp + 1] = mfma16x16x4d(ww[j].y, eb, F[2 * tp + 1]);
+            Br[2 * tp] = mfma16x16x4d(wr[j].x, eb, Br[2 * tp]);
+            Br[2 * tp + 1] = mfma16x16x4d(wr[j].y, eb, Br[2 * tp + 1]);
+            Bi[2 * tp] = mfma16x16x4d(wi[j].x, eb, Bi[2 * tp]);
+            Bi[2 * tp + 1] = mfma16x16x4d(wi[j].y, eb, Bi[2 * tp + 1]);
+          }
+        }
+      }
+    }
+  }
+  // Z = Y f + b at the lane's filter positions (every (observation, bin) of the tile belongs to exactly one lane)
+  const double sc = (OUT == 0) ? 1.0 / ssum : 1.0;
+  if ((OUT == 3 || OUT == 4) && wid == 0 && hq == 0 && col < rows) {
+    om[b0 + col] = m;
+    os[b0 + col] = ssum;
+  }
+  if constexpr (N == 256) {
+    double2 z[16];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double2 v = Trow[fpos(t, r)];
+        const double f = F[t][r] * sc;
+        z[4 * t + r] = make_double2(fma(v.x, f, Br[t][r] * sc), fma(v.y, f, Bi[t][r] * sc));
+      }
+    fft_pass_low4<true>(z, lg2, tw);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) Trow[16 * (hq + 4 * wid) + i] = z[i];
+    __syncthreads();
+    const int s1 = tid >> 4, g = tid & 15;
+    double2 x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = T[s1 * RS + g + 16 * i];
+    fft256_pass1<true>(x, lg2, g, tw);
+    if (s1 < rows) {
+      const long long o = (b0 + s1) * N + g;
+      if (OUT == 3) {
+        float2* at = reinterpret_cast<float2*>(oa) + o;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) at[16 * i] = make_float2((float)x[i].x, (float)x[i].y);
+      } else if (OUT == 4) {
+        double2* at = reinterpret_cast<double2*>(oa) + o;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) at[16 * i] = x[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) h[o + 16 * i] = x[i];
+      }
+    }
+  } else {
+    double2 z[4 * NTW];
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const double2 v = Trow[fpos(t, r)];
+        const double f = F[t][r] * sc;
+        z[4 * t + r] = make_double2(fma(v.x, f, Br[t][r] * sc), fma(v.y, f, Bi[t][r] * sc));
+      }
+    // a lane writes back only the positions it read (the last lp reads of the tile precede the chunk's barriers)
+#pragma unroll
+    for (int t = 0; t < NTW; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Trow[fpos(t, r)] = z[4 * t + r];
+    __syncthreads();
+    if (lg1 > 0) fft_axis_passes<true>(T, lgTS, RS, lgN, lg1, 1 << lg2, tw);
+    fft_axis_passes<true>(T, lgTS, RS, lgN, lg2, 1, tw);
+    if (OUT == 3) {
+      float2* at = reinterpret_cast<float2*>(oa) + b0 * N;
+      for (int e = tid; e < rows * N; e += 256) {
+        const double2 v = T[(e >> lgN) * RS + (e & (N - 1))];
+        at[e] = make_float2((float)v.x, (float)v.y);
+      }
+    } else if (OUT == 4) {
+      double2* at = reinterpret_cast<double2*>(oa) + b0 * N;
+      for (int e = tid; e < rows * N; e += 256) at[e] = T[(e >> lgN) * RS + (e & (N - 1))];
+    } else {
+      double2* ht = h + b0 * N;
+      for (int e = tid; e < rows * N; e += 256) ht[e] = T[(e >> lgN) * RS + (e & (N - 1))];
+    }
+  }
+}
+
 // natural-order per-bin tables of k_fft_prep -> the kernel's storage order (bit-reversed per axis),
 // negated rinv, components padded to Kp (padding: c' = -inf, zero tables); N <= 64: fragment order of
 // k_fft_wave, otherwise the row-major N x Kp / Kp x N order of k_fft_mfma
@@ -1547,7 +1862,7 @@ __global__ __launch_bounds__(256) void k_fft_pack(int N, int lg1, int lg2, int K
   // fragment order, table layouts: 0 k_fft_wave (lp bins 4 t + k, filter bins 16 t + row), 1 k_fft_chunk<256> (filter
   // bins chunk256_bin), 2 k_fft_wreg (lp bins 16 k + t, filter bins chunk256_bin)
   const int layout = (N == 256) ? 1 : (N == 64 && !has_mean && frag) ? 2 : 0;
-  if (N <= 64 || (!has_mean && frag)) {  // fragment order: e = ((cb Q + i) 64 + lane) 2 + s, Q = N / 8 16-byte loads per block and table
+  if (N <= 64 || frag) {  // fragment order: e = ((cb Q + i) 64 + lane) 2 + s, Q = N / 8 16-byte loads per block and table
     const int Q = N / 8, NT = N / 16;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
          e += (long long)gridDim.x * blockDim.x) {
@@ -1695,14 +2010,35 @@ hipError_t launch_chunk_t(const QceFftEstArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+template <int N, int OUT>
+hipError_t launch_chunk_hm(const QceFftEstArgs& a, hipStream_t st) {
+  constexpr size_t lds = FftChunkHmLds<N>::bytes;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_fft_chunk_hm<N, OUT>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int lg1 = __builtin_ctz(a.n1), lg2 = __builtin_ctz(a.n2);
+  dim3 grid((unsigned)((a.B + 15) / 16));
+  hipLaunchKernelGGL((k_fft_chunk_hm<N, OUT>), grid, dim3(256), lds, st, a.B, lg1, lg2, a.Kp, a.y, a.pr, a.pur, a.pui,
+                     a.pc, a.pw, a.pbr, a.pbi, a.h, a.om, a.os, a.oa);
+  return hipGetLastError();
+}
+
 template <int OUT, bool HM>
 hipError_t launch_mfma_out(const QceFftEstArgs& a, hipStream_t st) {
   switch (a.N) {
     case 16: return launch_wave_t<16, OUT, HM>(a, st);
     case 32: return launch_wave_t<32, OUT, HM>(a, st);
     case 64: return launch_wave_t<64, OUT, HM>(a, st);
-    case 128: return (!HM && a.chunk) ? launch_chunk_t<128, OUT>(a, st) : launch_mfma_t<128, OUT, HM>(a, st);
-    case 256: return (!HM && a.chunk) ? launch_chunk_t<256, OUT>(a, st) : launch_mfma_t<256, OUT, HM>(a, st);
+    case 128:
+      if (a.chunk) return HM ? launch_chunk_hm<128, OUT>(a, st) : launch_chunk_t<128, OUT>(a, st);
+      return launch_mfma_t<128, OUT, HM>(a, st);
+    case 256:
+      if (a.chunk) return HM ? launch_chunk_hm<256, OUT>(a, st) : launch_chunk_t<256, OUT>(a, st);
+      return launch_mfma_t<256, OUT, HM>(a, st);
     default: return hipErrorInvalidValue;
   }
 }

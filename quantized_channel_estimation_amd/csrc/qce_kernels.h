@@ -205,7 +205,7 @@ struct QceFftEstArgs {
   int Kp;
   const double *pr, *pur, *pui, *pc, *pw, *pbr, *pbi;
   int cu;     // compute units of the device (persistent grid of k_fft_wave)
-  int chunk;  // zero-mean N = 128, 256: k_fft_chunk on fragment-order tables (else k_fft_mfma, row-major)
+  int chunk;  // N = 128, 256: k_fft_chunk / k_fft_chunk_hm on fragment-order tables (else k_fft_mfma, row-major)
 };
 bool qce_fft_pow2(int v);
 int qce_fft_tile(int N, int K);  // 0: no tile fits (K too large)

@@ -94,7 +94,7 @@ struct qce_model {
   DevBuf<int> f_bad;
   DevBuf<double> f_pr, f_pur, f_pui, f_pc, f_pw, f_pbr, f_pbi;  // qce_fft_mfma.hip tables
   int fft_mfma = 0;                                            // the MFMA kernel serves 'all' / partial
-  int fft_chunk = 1;  // zero-mean N = 128, 256: k_fft_chunk (fragment-order tables); 0: k_fft_mfma (QCE_FFT_CHUNK=0)
+  int fft_chunk = 1;  // N = 128, 256: k_fft_chunk / k_fft_chunk_hm (fragment-order tables); 0: k_fft_mfma (QCE_FFT_CHUNK=0)
   // host-I/O pipeline of qce_estimate: two pinned slots per direction, copy-in / copy-out streams
   struct {
     double2* pin_y[2] = {nullptr, nullptr};

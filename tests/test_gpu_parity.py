@@ -466,17 +466,38 @@ def test_fourier_chunk_kernel(K, N, blocks, B, n_bits, monkeypatch):
     filter, two barriers per 128-component chunk) and k_fft_wreg (zero-mean N = 64) against the FP64 oracle and
     the kernels they replace (QCE_FFT_CHUNK=0: bin-split k_fft_mfma, LDS-transform k_fft_wave), 'all' mode and
     both K-shard partial accumulators."""
+    _chunk_vs_oracle(K, N, blocks, B, n_bits, False, monkeypatch)
+
+
+@pytest.mark.parametrize("K,N,blocks,B,n_bits", [
+    (128, 256, (4, 64), 1003, 2),   # cfg5 geometry with means
+    (200, 256, (16, 16), 517, 3),   # a second, partial chunk
+    (256, 128, (8, 16), 301, 2),    # two whole chunks
+    (130, 128, None, 250, np.inf),  # unquantised, a one-block second chunk
+    (7, 128, (2, 64), 33, 1),       # one padded block, three idle waves
+    (64, 256, None, 100, 2),        # circulant 256
+    (48, 256, (64, 4), 77, 2),      # n2 = 4
+    (128, 256, (4, 64), 5, 2),      # five observations
+])
+def test_fourier_chunk_kernel_means(K, N, blocks, B, n_bits, monkeypatch):
+    """k_fft_chunk_hm (N = 128, 256 with means: the mean terms 2 Re(Y^* u) in the log-probabilities and
+    sum_k gamma_k b_k in the filter, gmm_cplx_bussgang.py:256-264, :288) against the FP64 oracle and the bin-split
+    k_fft_mfma it replaces (QCE_FFT_CHUNK=0), 'all' mode and both K-shard partial accumulators."""
+    _chunk_vs_oracle(K, N, blocks, B, n_bits, True, monkeypatch)
+
+
+def _chunk_vs_oracle(K, N, blocks, B, n_bits, mean, monkeypatch):
     _gpu_or_skip()
     from oracle import qce_oracle as O
     from quantized_channel_estimation_amd import _lib, inputs
     from quantized_channel_estimation_amd.sharding import combine_partials_numpy
     cov = "circulant" if blocks is None else "block-circulant"
     means, covs, w = inputs.synthetic_model(K, N, cov_type=cov, seed=K + 1, blocks=blocks)
-    means = np.zeros_like(means)
     rng = np.random.default_rng(K * N)
+    means = 0.3 * inputs.crandn(K, N, rng=rng) if mean else np.zeros_like(means)
     h, _ = inputs.scm_generate(B, 1, N, rng, n_path=3)
     qz = (None, None, None)
-    if n_bits != 1:
+    if n_bits not in (1, np.inf):
         qz = inputs.get_quantizer([5.0], n_bits, "uniform")[5.0]
     y = inputs.get_observation_nbit(h[:, 0, :].astype(complex), 5.0, None, n_bits, qz[0], qz[1], rng=rng)
     out = {}
