@@ -399,8 +399,8 @@ def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
 def fourier_kernel(N, has_mean):
     """The Fourier-path kernel qce_fft_mfma.hip runs for this shape (QCE_FFT_CHUNK=0 selects the round-2 kernels)."""
     new = os.environ.get("QCE_FFT_CHUNK", "1") != "0"
-    if N == 64 and new and not has_mean:
-        return "k_fft_wreg"
+    if N == 64 and new:
+        return "k_fft_wreg<HM>" if has_mean else "k_fft_wreg"
     if N <= 64:
         return "k_fft_wave"
     if not new:

@@ -7,11 +7,11 @@
 // result keeps the FP64 accuracy of the reference (gmm_cplx_bussgang.py computes in complex128).
 //
 // Kernels (dispatch in launch_mfma_out; QCE_FFT_CHUNK=0 at prepare time keeps the round-2 pair):
-//   k_fft_wreg   zero-mean N = 64: persistent one-wave tiles, register transform (pass 1 / LDS exchange / pass 2)
+//   k_fft_wreg   N = 64: persistent one-wave tiles, register transform (pass 1 / LDS exchange / pass 2); <HM> means
 //   k_fft_chunk  zero-mean N = 128, 256: components split over the waves for lp / softmax, bins for the filter,
 //                two barriers per 128-component chunk; register transform for N = 256
 //   k_fft_chunk_hm  N = 128, 256 with means: k_fft_chunk's split, spectra kept in the LDS tile, 3x the MFMAs
-//   k_fft_wave   N = 16, 32 and models with means up to 64 (wave-local LDS transform)
+//   k_fft_wave   N = 16, 32 (wave-local LDS transform; N = 64 with QCE_FFT_CHUNK=0)
 //   k_fft_mfma   N = 128, 256 with QCE_FFT_CHUNK=0 (the round-2 kernel, described next)
 // On gfx950 FP64 VALU instructions and FP64 MFMAs share the SIMD's issue budget (tools/probe/f64_pipe_probe.hip),
 // so the newer kernels are organised around fewer VALU instructions per MFMA.
@@ -941,19 +941,30 @@ QCE_DEV int chunk256_bin(int t, int row) { return (((row & 3) + 4 * (t >> 2)) <<
 // 16 hq + u (the B operand |Y|^2 comes from registers, computed once per tile), filter tile t, row hq + 4 r =
 // position 16 hq + r + 4 t (chunk256_bin).  The spectra wait in the lane's own slots of the wave tile during the
 // component loop; Z, inverse pass 2, the exchange and inverse pass 1 run the same way back, stores from registers.
-template <int OUT>
-__global__ __launch_bounds__(256, 2) void k_fft_wreg(long long B, long long ntiles, int lg2, int Kp,
-                                                     const double2* __restrict__ y, const double* __restrict__ pr,
-                                                     const double* __restrict__ pc, const double* __restrict__ pw,
-                                                     double2* __restrict__ h, double* __restrict__ om,
-                                                     double* __restrict__ os, float* __restrict__ oa) {
+// HM (models with means, gmm_cplx_bussgang.py:96-100, :256-264, :288): lp k-step u adds 2 Re(Y_u^* u_k,u) as two more
+// MFMAs on the lane's own spectra (Re Y, Im Y of position 16 hq + u; a second accumulator), the filter two more
+// accumulator sets (Re b, Im b) at the filter positions, Z = Y f + b: 3x the MFMAs, one wave per SIMD (512
+// registers) and a larger per-wave LDS slot for the tail's partial exchange.
+template <int OUT, bool HM>
+__global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wreg(long long B, long long ntiles, int lg2, int Kp,
+                                                              const double2* __restrict__ y,
+                                                              const double* __restrict__ pr,
+                                                              const double* __restrict__ pur,
+                                                              const double* __restrict__ pui,
+                                                              const double* __restrict__ pc,
+                                                              const double* __restrict__ pw,
+                                                              const double* __restrict__ pbr,
+                                                              const double* __restrict__ pbi,
+                                                              double2* __restrict__ h, double* __restrict__ om,
+                                                              double* __restrict__ os, float* __restrict__ oa) {
   constexpr int N = 64, NT = 4, NL = 8, NW = 8, RS = N + 1;
+  constexpr int WS = HM ? 1664 : 16 * RS;  // double2 per wave slot: the tile, or the tail's (F, Br, Bi, m, s) rows
   extern __shared__ __attribute__((aligned(16))) char smem[];
   double2* tw = reinterpret_cast<double2*>(smem);
   const int tid = threadIdx.x;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   double* etab = reinterpret_cast<double*>(tw + 128);  // 2^(j/32), j < 32
-  double2* T = tw + 128 + 16 + wid * (16 * RS);
+  double2* T = tw + 128 + 16 + wid * WS;
   for (int t = tid; t < 128; t += 256) {
     double sn, cs;
     sincospi(-(double)t / 128.0, &sn, &cs);
@@ -968,6 +979,10 @@ __global__ __launch_bounds__(256, 2) void k_fft_wreg(long long B, long long ntil
   // tables, y and h through buffer descriptors (scalar registers); per-lane 32-bit offsets
   const __amdgpu_buffer_rsrc_t rpr = buf_rsrc(pr, (unsigned)(Kp * N * 8)), rpw = buf_rsrc(pw, (unsigned)(Kp * N * 8));
   const __amdgpu_buffer_rsrc_t rpc = buf_rsrc(pc, (unsigned)(Kp * 8));
+  const __amdgpu_buffer_rsrc_t rur = buf_rsrc(pur, HM ? (unsigned)(Kp * N * 8) : 0u);
+  const __amdgpu_buffer_rsrc_t rui = buf_rsrc(pui, HM ? (unsigned)(Kp * N * 8) : 0u);
+  const __amdgpu_buffer_rsrc_t rbr = buf_rsrc(pbr, HM ? (unsigned)(Kp * N * 8) : 0u);
+  const __amdgpu_buffer_rsrc_t rbi = buf_rsrc(pbi, HM ? (unsigned)(Kp * N * 8) : 0u);
   const unsigned ul16 = (unsigned)lane * 16;
   const unsigned yo = (unsigned)(s0 * N + g1) * 16;  // pass-1 lane: byte offset of (s0, g1) in a tile
   FW_STAMP_DECL
@@ -1010,12 +1025,19 @@ __global__ __launch_bounds__(256, 2) void k_fft_wreg(long long B, long long ntil
       return q.x * q.x + q.y * q.y;
     };
     FW_STAMP(1);
-    f64x4 F[NT];
+    f64x4 F[NT], Br[HM ? NT : 1], Bi[HM ? NT : 1];
 #pragma unroll
     for (int t = 0; t < NT; ++t)
       for (int r = 0; r < 4; ++r) F[t][r] = 0.0;
+    if constexpr (HM) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+        for (int r = 0; r < 4; ++r) Br[t][r] = Bi[t][r] = 0.0;
+    }
     double m = -__builtin_inf(), ssum = 0.0;
     // c'_comp is added after the MFMAs, so its loads have the whole product to land
+    // HM: the mean tables of a block are loaded at its start and consumed after its |Y|^2 (lp) or w (filter) MFMAs,
+    // which cover their latency; only the r / w tables are prefetched a block ahead (register budget)
     auto lp_block = [&](int cb, const double2* ta) {
       double pcv[4];
 #pragma unroll
@@ -1025,10 +1047,33 @@ __global__ __launch_bounds__(256, 2) void k_fft_wreg(long long B, long long ntil
       for (int r = 0; r < 4; ++r) C[r] = 0.0;
       unsigned o = 0;  // opaque zero: the spectra reads stay in the loop instead of being hoisted into registers
       asm volatile("" : "+v"(o));
+      double2 ua[HM ? NL : 1], qa[HM ? NL : 1];
+      if constexpr (HM) {
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+          ua[i] = buf_ld2(rur, ul16, (unsigned)cb * NL * 1024 + 1024 * i);
+          qa[i] = buf_ld2(rui, ul16, (unsigned)cb * NL * 1024 + 1024 * i);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < NL; ++i) {
         C = mfma16x16x4d(ta[i].x, y2(2 * i, o), C);
         C = mfma16x16x4d(ta[i].y, y2(2 * i + 1, o), C);
+      }
+      if constexpr (HM) {  // + 2 Re(Y^* u): (2 Re u) Re Y + (2 Im u) Im Y on the lane's own points
+        f64x4 D;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) D[r] = 0.0;
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+          const double2 q0 = Town[2 * i + o], q1 = Town[2 * i + 1 + o];
+          D = mfma16x16x4d(ua[i].x, q0.x, D);
+          D = mfma16x16x4d(qa[i].x, q0.y, D);
+          D = mfma16x16x4d(ua[i].y, q1.x, D);
+          D = mfma16x16x4d(qa[i].y, q1.y, D);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) C[r] += D[r];
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) C[r] += pcv[r];
@@ -1047,6 +1092,13 @@ __global__ __launch_bounds__(256, 2) void k_fft_wreg(long long B, long long ntil
         ssum *= alpha;
 #pragma unroll
         for (int t = 0; t < NT; ++t) F[t] *= alpha;
+        if constexpr (HM) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            Br[t] *= alpha;
+            Bi[t] *= alpha;
+          }
+        }
         m = mn;
       }
       const double sh = (m == -__builtin_inf()) ? 0.0 : m;
@@ -1054,12 +1106,32 @@ __global__ __launch_bounds__(256, 2) void k_fft_wreg(long long B, long long ntil
       for (int r = 0; r < 4; ++r) e[r] = exp_nonpos(C[r] - sh, etab);
       ssum += (e[0] + e[1]) + (e[2] + e[3]);
     };
-    auto filter_block = [&](const double2* tb, const double* e) {
+    auto filter_block = [&](const double2* tb, int cb, const double* e) {
+      double2 tr[HM ? NW : 1], ti[HM ? NW : 1];
+      if constexpr (HM) {
+#pragma unroll
+        for (int i = 0; i < NW; ++i) {
+          tr[i] = buf_ld2(rbr, ul16, (unsigned)cb * NW * 1024 + 1024 * i);
+          ti[i] = buf_ld2(rbi, ul16, (unsigned)cb * NW * 1024 + 1024 * i);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 4 * NT; ++j) {
         const int r = j / NT, t = j % NT;
         const double wv = (j & 1) ? tb[j >> 1].y : tb[j >> 1].x;
         F[t] = mfma16x16x4d(wv, e[r], F[t]);
+      }
+      if constexpr (HM) {
+#pragma unroll
+        for (int j = 0; j < 4 * NT; ++j) {
+          const int r = j / NT, t = j % NT;
+          Br[t] = mfma16x16x4d((j & 1) ? tr[j >> 1].y : tr[j >> 1].x, e[r], Br[t]);
+        }
+#pragma unroll
+        for (int j = 0; j < 4 * NT; ++j) {
+          const int r = j / NT, t = j % NT;
+          Bi[t] = mfma16x16x4d((j & 1) ? ti[j >> 1].y : ti[j >> 1].x, e[r], Bi[t]);
+        }
       }
     };
     const int nb = (ncb - s0b + bs - 1) / bs;  // this wave's component blocks s0b + j bs, j < nb
@@ -1067,27 +1139,27 @@ __global__ __launch_bounds__(256, 2) void k_fft_wreg(long long B, long long ntil
     if (nb > 0) {
       const int last = nb - 1;
       double2 ta[NL], tb[NW];
+      auto load_lp = [&](int cb) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < NL; ++i) ta[i] = buf_ld2(rpr, ul16, (unsigned)blk(0) * NL * 1024 + 1024 * i);
+        for (int i = 0; i < NL; ++i) ta[i] = buf_ld2(rpr, ul16, (unsigned)cb * NL * 1024 + 1024 * i);
+      };
+      auto load_w = [&](int cb) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < NW; ++i) tb[i] = buf_ld2(rpw, ul16, (unsigned)cb * NW * 1024 + 1024 * i);
+      };
+      load_lp(blk(0));
       f64x4 C = lp_block(blk(0), ta);
-      {
-        const int b1 = blk(last > 0 ? 1 : 0);
-#pragma unroll
-        for (int i = 0; i < NL; ++i) ta[i] = buf_ld2(rpr, ul16, (unsigned)b1 * NL * 1024 + 1024 * i);
-#pragma unroll
-        for (int i = 0; i < NW; ++i) tb[i] = buf_ld2(rpw, ul16, (unsigned)blk(0) * NW * 1024 + 1024 * i);
-      }
+      load_lp(blk(last > 0 ? 1 : 0));
+      load_w(blk(0));
       FW_STAMP(2);
       for (int j = 0; j < last; ++j) {
         const int b1 = blk(j + 1), b2 = blk(j + 2 < last ? j + 2 : last);
         const f64x4 Cn = lp_block(b1, ta);
-#pragma unroll
-        for (int i = 0; i < NL; ++i) ta[i] = buf_ld2(rpr, ul16, (unsigned)b2 * NL * 1024 + 1024 * i);
+        load_lp(b2);
         double e[4];
         softmax(C, e);
-        filter_block(tb, e);
-#pragma unroll
-        for (int i = 0; i < NW; ++i) tb[i] = buf_ld2(rpw, ul16, (unsigned)b1 * NW * 1024 + 1024 * i);
+        filter_block(tb, blk(j), e);
+        load_w(b1);
         C = Cn;
       }
       FW_STAMP(3);
@@ -1095,42 +1167,62 @@ __global__ __launch_bounds__(256, 2) void k_fft_wreg(long long B, long long ntil
       {
         double e[4];
         softmax(C, e);
-        filter_block(tb, e);
+        filter_block(tb, blk(last), e);
       }
     }
     ssum = col_sum4(ssum);  // the lanes' partial sums -> the column's (bit-identical in its four lanes)
     if (coop) {  // waves 1-3 hand (F, m, s) to wave 0 through their own tiles (wave 0's holds its spectra)
       double* Td = reinterpret_cast<double*>(T);
+      constexpr int NA = HM ? 3 : 1;  // accumulator sets: F (, Br, Bi)
       if (wid != 0) {
 #pragma unroll
         for (int t = 0; t < NT; ++t)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) Td[(t * 4 + r) * 64 + lane] = F[t][r];
-        Td[4 * NT * 64 + lane] = m;
-        Td[(4 * NT + 1) * 64 + lane] = ssum;
+          for (int r = 0; r < 4; ++r) {
+            Td[(t * 4 + r) * 64 + lane] = F[t][r];
+            if constexpr (HM) {
+              Td[(4 * NT + t * 4 + r) * 64 + lane] = Br[t][r];
+              Td[(8 * NT + t * 4 + r) * 64 + lane] = Bi[t][r];
+            }
+          }
+        Td[NA * 4 * NT * 64 + lane] = m;
+        Td[(NA * 4 * NT + 1) * 64 + lane] = ssum;
       }
       __syncthreads();
       if (wid == 0) {  // fixed order: wave 0's own partial, then waves 1, 2, 3
         double mm = m;
 #pragma unroll
         for (int w = 1; w < 4; ++w) {
-          const double* Tw = reinterpret_cast<const double*>(tw + 128 + 16 + w * (16 * RS));
-          mm = fmax(mm, Tw[4 * NT * 64 + lane]);
+          const double* Tw = reinterpret_cast<const double*>(tw + 128 + 16 + w * WS);
+          mm = fmax(mm, Tw[NA * 4 * NT * 64 + lane]);
         }
         const double f0 = exp_nonpos(m - mm, etab);
         ssum *= f0;
 #pragma unroll
         for (int t = 0; t < NT; ++t) F[t] *= f0;
+        if constexpr (HM) {
+#pragma unroll
+          for (int t = 0; t < NT; ++t) {
+            Br[t] *= f0;
+            Bi[t] *= f0;
+          }
+        }
 #pragma unroll
         for (int w = 1; w < 4; ++w) {
-          const double* Tw = reinterpret_cast<const double*>(tw + 128 + 16 + w * (16 * RS));
-          const double mw = Tw[4 * NT * 64 + lane];
+          const double* Tw = reinterpret_cast<const double*>(tw + 128 + 16 + w * WS);
+          const double mw = Tw[NA * 4 * NT * 64 + lane];
           const double fw = exp_nonpos(mw - mm, etab);
-          ssum = fma(Tw[(4 * NT + 1) * 64 + lane], fw, ssum);
+          ssum = fma(Tw[(NA * 4 * NT + 1) * 64 + lane], fw, ssum);
 #pragma unroll
           for (int t = 0; t < NT; ++t)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) F[t][r] = fma(Tw[(t * 4 + r) * 64 + lane], fw, F[t][r]);
+            for (int r = 0; r < 4; ++r) {
+              F[t][r] = fma(Tw[(t * 4 + r) * 64 + lane], fw, F[t][r]);
+              if constexpr (HM) {
+                Br[t][r] = fma(Tw[(4 * NT + t * 4 + r) * 64 + lane], fw, Br[t][r]);
+                Bi[t][r] = fma(Tw[(8 * NT + t * 4 + r) * 64 + lane], fw, Bi[t][r]);
+              }
+            }
         }
         m = mm;
       }
@@ -1148,7 +1240,10 @@ __global__ __launch_bounds__(256, 2) void k_fft_wreg(long long B, long long ntil
         for (int r = 0; r < 4; ++r) {
           const double2 q = Town[r + 4 * t];
           const double f = F[t][r] * sc;
-          z[r + 4 * t] = make_double2(q.x * f, q.y * f);
+          if constexpr (HM)
+            z[r + 4 * t] = make_double2(fma(q.x, f, Br[t][r] * sc), fma(q.y, f, Bi[t][r] * sc));
+          else
+            z[r + 4 * t] = make_double2(q.x * f, q.y * f);
         }
       FW_STAMP(4);
       fft_pass_low4<true>(z, lg2, tw);
@@ -1861,7 +1956,7 @@ __global__ __launch_bounds__(256) void k_fft_pack(int N, int lg1, int lg2, int K
   const long long total = (long long)N * Kp;
   // fragment order, table layouts: 0 k_fft_wave (lp bins 4 t + k, filter bins 16 t + row), 1 k_fft_chunk<256> (filter
   // bins chunk256_bin), 2 k_fft_wreg (lp bins 16 k + t, filter bins chunk256_bin)
-  const int layout = (N == 256) ? 1 : (N == 64 && !has_mean && frag) ? 2 : 0;
+  const int layout = (N == 256) ? 1 : (N == 64 && frag) ? 2 : 0;
   if (N <= 64 || frag) {  // fragment order: e = ((cb Q + i) 64 + lane) 2 + s, Q = N / 8 16-byte loads per block and table
     const int Q = N / 8, NT = N / 16;
     for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
@@ -1966,28 +2061,29 @@ hipError_t launch_wave_c(const QceFftEstArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-template <int OUT>
+template <int OUT, bool HM>
 hipError_t launch_wreg(const QceFftEstArgs& a, hipStream_t st) {
-  const size_t lds = 128 * 16 + 32 * 8 + (size_t)4 * 16 * 65 * 16;
+  const size_t lds = 128 * 16 + 32 * 8 + (size_t)4 * (HM ? 1664 : 16 * 65) * 16;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_fft_wreg<OUT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute((const void*)k_fft_wreg<OUT, HM>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)lds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const long long ntiles = (a.B + 15) / 16;
-  const long long slots = 2LL * (a.cu > 0 ? a.cu : 256);  // persistent: two workgroups (8 waves) per CU
+  // persistent: two workgroups (8 waves) per CU, one with means (a wave per SIMD)
+  const long long slots = (HM ? 1LL : 2LL) * (a.cu > 0 ? a.cu : 256);
   const long long wgs = ntiles < slots ? ntiles : slots;
-  hipLaunchKernelGGL((k_fft_wreg<OUT>), dim3((unsigned)wgs), dim3(256), lds, st, a.B, ntiles, __builtin_ctz(a.n2), a.Kp,
-                     a.y, a.pr, a.pc, a.pw, a.h, a.om, a.os, a.oa);
+  hipLaunchKernelGGL((k_fft_wreg<OUT, HM>), dim3((unsigned)wgs), dim3(256), lds, st, a.B, ntiles, __builtin_ctz(a.n2),
+                     a.Kp, a.y, a.pr, a.pur, a.pui, a.pc, a.pw, a.pbr, a.pbi, a.h, a.om, a.os, a.oa);
   return hipGetLastError();
 }
 
 template <int N, int OUT, bool HM>
 hipError_t launch_wave_t(const QceFftEstArgs& a, hipStream_t st) {
-  if constexpr (N == 64 && !HM) {
-    if (a.chunk) return launch_wreg<OUT>(a, st);
+  if constexpr (N == 64) {
+    if (a.chunk) return launch_wreg<OUT, HM>(a, st);
   }
   return a.n1 == 1 ? launch_wave_c<N, OUT, HM, true>(a, st) : launch_wave_c<N, OUT, HM, false>(a, st);
 }

@@ -478,11 +478,17 @@ def test_fourier_chunk_kernel(K, N, blocks, B, n_bits, monkeypatch):
     (64, 256, None, 100, 2),        # circulant 256
     (48, 256, (64, 4), 77, 2),      # n2 = 4
     (128, 256, (4, 64), 5, 2),      # five observations
+    # N = 64: k_fft_wreg<HM>
+    (128, 64, None, 3001, 3),       # cfg3 geometry with means
+    (64, 64, (2, 32), 500, 2),
+    (40, 64, (16, 4), 300, 1),      # n2 = 4
+    (128, 64, None, 1, 3),          # one observation
 ])
 def test_fourier_chunk_kernel_means(K, N, blocks, B, n_bits, monkeypatch):
     """k_fft_chunk_hm (N = 128, 256 with means: the mean terms 2 Re(Y^* u) in the log-probabilities and
-    sum_k gamma_k b_k in the filter, gmm_cplx_bussgang.py:256-264, :288) against the FP64 oracle and the bin-split
-    k_fft_mfma it replaces (QCE_FFT_CHUNK=0), 'all' mode and both K-shard partial accumulators."""
+    sum_k gamma_k b_k in the filter, gmm_cplx_bussgang.py:256-264, :288) and k_fft_wreg<HM> (N = 64 with means)
+    against the FP64 oracle and the kernels they replace (QCE_FFT_CHUNK=0: bin-split k_fft_mfma, LDS-transform
+    k_fft_wave), 'all' mode and both K-shard partial accumulators."""
     _chunk_vs_oracle(K, N, blocks, B, n_bits, True, monkeypatch)
 
 
@@ -522,6 +528,7 @@ def _chunk_vs_oracle(K, N, blocks, B, n_bits, mean, monkeypatch):
     (64, 64, (8, 8), 70013, 1, "uniform", False),  # 2-D transform through the same phases
     (16, 16, (4, 4), 40013, 2, "uniform", False),
     (32, 32, None, 20013, np.inf, "uniform", True),  # with means: every tile one wave, persistent loop
+    (128, 64, None, 40013, 3, "lloyd", True),  # cfg3 with means: k_fft_wreg<HM>, one workgroup per CU
 ])
 def test_fourier_wave_kernel_persistent_phases(K, N, blocks, B, n_bits, qtype, mean, monkeypatch):
     """k_fft_wave (N <= 64) at batches large enough for its main phase: one wave per 16-row tile over
@@ -550,7 +557,8 @@ def test_fourier_wave_kernel_persistent_phases(K, N, blocks, B, n_bits, qtype, m
     assert hg.shape == (B, N) and np.isfinite(hg).all()
     tol = 1e-9 if n_bits != 1 else 1e-7
     ntiles = (B + 15) // 16
-    edge = (ntiles // 2048) * 2048 * 16  # main/tail boundary at 256 CUs x 2 workgroups x 4 waves
+    per_round = 1024 if (N == 64 and mean) else 2048  # 256 CUs x 2 workgroups (1 for k_fft_wreg<HM>) x 4 waves
+    edge = (ntiles // per_round) * per_round * 16  # main/tail boundary
     for lo, hi in ((0, 200), (max(edge - 100, 0), edge + 100), (B - 200, B)):
         ho = O.estimate(means, covs, w, y[lo:hi], 5.0, N, None, "all", n_bits, qtype, qz)
         assert rel_fro(hg[lo:hi], ho) < tol, (lo, hi, rel_fro(hg[lo:hi], ho))
