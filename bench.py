@@ -98,7 +98,7 @@ def parse():
                          "timing, rank 0 prints one JSON line; no GPU is touched")
     ap.add_argument("--traffic", default=None,
                     help="JSON with PMC-derived HBM bytes per launch of the estimate kernel "
-                         "(default profiles/traffic_<config>.json)")
+                         "(default profiles/traffic_<config>.json, traffic_<config>_mean.json with --mean)")
     a = ap.parse_args()
     if a.shard is None:
         a.shard = DEFAULT_SHARD[a.config]
@@ -713,7 +713,8 @@ def main():
     k_local = (lambda s: s[1] - s[0])(component_slices(K, world)[rank]) if kshard else K
     kern_tag = "fft" if dm.structure()[2] else ("f64" if dtype_of(dm) == "f64" else "h2")
     traffic = None
-    tpath = args.traffic or os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
+    tpath = args.traffic or os.path.join(ROOT, "profiles",
+                                         f"traffic_{args.config}{'_mean' if args.mean else ''}.json")
     traffic_note = None
     if os.path.exists(tpath):
         try:

@@ -34,6 +34,11 @@
 #include "qce_common.h"
 #include "qce_kernels.h"
 
+// 1: pass-1 twiddles from the conflict-free lane table (pass1_lane_tw); 0: from the 128-entry table (A/B builds)
+#ifndef QCE_FFT_LANE_TW
+#define QCE_FFT_LANE_TW 1
+#endif
+
 namespace {
 
 constexpr double SQH = 0.70710678118654752440;  // sqrt(1/2)
@@ -829,14 +834,15 @@ QCE_DEV double2 root_any(double2 v, int P, int mm) {
 // half-distance 2^lgD (axis units), j = the axis position bits below the range (the group twiddle W_{2D_s}^j;
 // JZ: j == 0 for every thread).  Forward: DIF stages, inverse: the same stages reversed (DIT), conjugate twiddles --
 // the arithmetic of fft_pass with all R elements in one thread.
-template <int RL, bool INV, int S, bool JZ>
+// LT: tw is a pass-1 lane table (pass1_lane_tw) and j the lane's g: stage sI's twiddle is tw[16 sI + g].
+template <int RL, bool INV, int S, bool JZ, bool LT = false>
 QCE_DEV void reg_group(double2* x, int lgD, int j, const double2* tw) {
   constexpr int R = 1 << RL;
   double2 w[RL];
   if constexpr (!JZ) {
 #pragma unroll
     for (int sI = 0; sI < RL; ++sI) {
-      w[sI] = tw[j << (7 - (lgD - sI))];
+      w[sI] = LT ? tw[16 * sI + j] : tw[j << (7 - (lgD - sI))];
       if (INV) w[sI].y = -w[sI].y;
     }
   }
@@ -874,47 +880,68 @@ QCE_DEV void reg_group(double2* x, int lgD, int j, const double2* tw) {
 
 // One pass over a thread's 2^RT points (array index = RT bits of the storage position): array bits [0, RA) are
 // axis n2 (segment A), [RA, RT) axis n1 (segment B).  The axes are independent, so the segments run in either order.
-template <int RT, int RA, bool INV, bool JZA, bool JZB>
+template <int RT, int RA, bool INV, bool JZA, bool JZB, bool LT = false>
 QCE_DEV void reg_pass(double2* x, int lgDA, int jA, int lgDB, int jB, const double2* tw) {
   constexpr int RB = RT - RA;
   if constexpr (RB > 0) {
 #pragma unroll
-    for (int a = 0; a < (1 << RA); ++a) reg_group<RB, INV, (1 << RA), JZB>(x + a, lgDB, jB, tw);
+    for (int a = 0; a < (1 << RA); ++a) reg_group<RB, INV, (1 << RA), JZB, LT>(x + a, lgDB, jB, tw);
   }
   if constexpr (RA > 0) {
 #pragma unroll
-    for (int b = 0; b < (1 << RB); ++b) reg_group<RA, INV, 1, JZA>(x + (b << RA), lgDA, jA, tw);
+    for (int b = 0; b < (1 << RB); ++b) reg_group<RA, INV, 1, JZA, LT>(x + (b << RA), lgDA, jA, tw);
   }
 }
-template <int RA, bool INV, bool JZA, bool JZB>
+template <int RA, bool INV, bool JZA, bool JZB, bool LT = false>
 QCE_DEV void reg_pass16(double2 (&x)[16], int lgDA, int jA, int lgDB, int jB, const double2* tw) {
-  reg_pass<4, RA, INV, JZA, JZB>(x, lgDA, jA, lgDB, jB, tw);
+  reg_pass<4, RA, INV, JZA, JZB, LT>(x, lgDA, jA, lgDB, jB, tw);
+}
+
+// Pass-1 lane twiddle table (64 double2): entry 16 sI + g = the stage-sI group twiddle of the lanes whose pass-1
+// points have low bits g.  Pass 1 reads tw[j << (7 - (lgD - sI))] with j = g (or g >> lg2): the 16 lanes of a
+// ds_read_b128 group (distinct g) land on only 2-8 of the 128-entry table's bank quads (4- to 8-way conflicts,
+// a quarter of the Fourier kernels' LDS cycles); the lane table puts them on 16 consecutive 16-byte slots.  The
+// entries are computed like tw (same sincospi of the same index), so both forms are bit-identical.  The non-JZ
+// segment of pass 1 is n2 bits [4, lg2) (j = g, lgD = lg2 - 1) for lg2 > 4, else n1 bits [4, lgN) (j = g >> lg2,
+// lgD = lgN - 1 - lg2); threads 0-63 fill it.
+QCE_DEV void pass1_lane_tw(double2* tl, int lgN, int lg2, int tid) {
+  if (tid >= 64) return;
+  const int sI = tid >> 4, g = tid & 15;
+  const int RL = lg2 > 4 ? lg2 - 4 : (lg2 == 4 ? 0 : lgN - 4);
+  const int lgD = lg2 > 4 ? lg2 - 1 : lgN - 1 - lg2;
+  const int j = lg2 > 4 ? g : (g >> lg2);
+  double sn = 0.0, cs = 1.0;
+  if (sI < RL) sincospi(-(double)(j << (7 - (lgD - sI))) / 128.0, &sn, &cs);
+  tl[tid] = make_double2(cs, sn);
 }
 
 // N = 64 = n1 n2: pass 1 = storage bits 5, 4 on a group of 4 points sharing the bits 0-3 (g); segment A = n2 bits
 // [4, min(lg2, 6)), B = n1 bits [max(lg2, 4), 6), j = the axis bits below the segment
-template <bool INV>
+// LT: tw is the pass-1 lane table (pass1_lane_tw with lgN = 6)
+template <bool INV, bool LT = false>
 QCE_DEV void fft64_pass1(double2* x, int lg2, int g, const double2* tw) {
   switch (lg2) {
-    case 6: reg_pass<2, 2, INV, false, true>(x, 5, g, 0, 0, tw); break;
-    case 5: reg_pass<2, 1, INV, false, true>(x, 4, g, 0, 0, tw); break;
-    case 4: reg_pass<2, 0, INV, true, true>(x, 0, 0, 1, 0, tw); break;
-    default: reg_pass<2, 0, INV, true, false>(x, 0, 0, 5 - lg2, g >> lg2, tw); break;
+    case 6: reg_pass<2, 2, INV, false, true, LT>(x, 5, g, 0, 0, tw); break;
+    case 5: reg_pass<2, 1, INV, false, true, LT>(x, 4, g, 0, 0, tw); break;
+    case 4: reg_pass<2, 0, INV, true, true, LT>(x, 0, 0, 1, 0, tw); break;
+    default: reg_pass<2, 0, INV, true, false, LT>(x, 0, 0, 5 - lg2, LT ? g : g >> lg2, tw); break;
   }
 }
 
 // N = 256 = n1 n2 (lg2 = log2 n2): the forward transform's stages in descending storage bit order are bits 7..4
 // (pass 1) and 3..0 (pass 2) -- per axis high bits before low bits, as DIF requires.  Pass 1: the thread's points
 // share the storage bits 0-3 (g), pass 2 the bits 4-7.
-template <bool INV>
+template <bool INV, bool LT = false>  // LT: tw is the pass-1 lane table (pass1_lane_tw with lgN = 8)
 QCE_DEV void fft256_pass1(double2 (&x)[16], int lg2, int g, const double2* tw) {
   switch (lg2) {  // segment A = n2 bits [4, lg2), B = n1 bits [max(lg2, 4), 8)
-    case 8: reg_pass16<4, INV, false, true>(x, 7, g, 0, 0, tw); break;
-    case 7: reg_pass16<3, INV, false, true>(x, 6, g, 0, 0, tw); break;
-    case 6: reg_pass16<2, INV, false, true>(x, 5, g, 1, 0, tw); break;
-    case 5: reg_pass16<1, INV, false, true>(x, 4, g, 2, 0, tw); break;
-    case 4: reg_pass16<0, INV, true, true>(x, 0, 0, 3, 0, tw); break;
-    default: reg_pass16<0, INV, true, false>(x, 0, 0, 7 - lg2, g >> lg2, tw); break;  // n1 bits 4-7, j = n1 bits < 4
+    case 8: reg_pass16<4, INV, false, true, LT>(x, 7, g, 0, 0, tw); break;
+    case 7: reg_pass16<3, INV, false, true, LT>(x, 6, g, 0, 0, tw); break;
+    case 6: reg_pass16<2, INV, false, true, LT>(x, 5, g, 1, 0, tw); break;
+    case 5: reg_pass16<1, INV, false, true, LT>(x, 4, g, 2, 0, tw); break;
+    case 4: reg_pass16<0, INV, true, true, LT>(x, 0, 0, 3, 0, tw); break;
+    default:  // n1 bits 4-7, j = n1 bits < 4
+      reg_pass16<0, INV, true, false, LT>(x, 0, 0, 7 - lg2, LT ? g : g >> lg2, tw);
+      break;
   }
 }
 // pass 2 of every N >= 16 split: storage bits 3..0 of a lane's 16 points (bits >= 4 fixed)
@@ -964,13 +991,15 @@ __global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wreg(long long B, long 
   const int tid = threadIdx.x;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   double* etab = reinterpret_cast<double*>(tw + 128);  // 2^(j/32), j < 32
-  double2* T = tw + 128 + 16 + wid * WS;
+  double2* tl = tw + 144;                               // pass-1 lane twiddles
+  double2* T = tw + 208 + wid * WS;
   for (int t = tid; t < 128; t += 256) {
     double sn, cs;
     sincospi(-(double)t / 128.0, &sn, &cs);
     tw[t] = make_double2(cs, sn);
   }
   exp2_tab_init(etab, tid);
+  pass1_lane_tw(tl, 6, lg2, tid);
   __syncthreads();
   const int col = lane & 15, hq = lane >> 4;
   const int g1 = lane & 15, s0 = lane >> 4;  // pass-1 lane: observations s0 + 4 q, positions g1 + 16 j
@@ -1004,7 +1033,7 @@ __global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wreg(long long B, long 
     if (coop) load_y(tile);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      fft64_pass1<false>(v + 4 * q, lg2, g1, tw);
+      fft64_pass1<false, QCE_FFT_LANE_TW>(v + 4 * q, lg2, g1, QCE_FFT_LANE_TW ? tl : tw);
 #pragma unroll
       for (int j = 0; j < 4; ++j) T[(s0 + 4 * q) * RS + g1 + 16 * j] = v[4 * q + j];
     }
@@ -1193,7 +1222,7 @@ __global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wreg(long long B, long 
         double mm = m;
 #pragma unroll
         for (int w = 1; w < 4; ++w) {
-          const double* Tw = reinterpret_cast<const double*>(tw + 128 + 16 + w * WS);
+          const double* Tw = reinterpret_cast<const double*>(tw + 208 + w * WS);
           mm = fmax(mm, Tw[NA * 4 * NT * 64 + lane]);
         }
         const double f0 = exp_nonpos(m - mm, etab);
@@ -1209,7 +1238,7 @@ __global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wreg(long long B, long 
         }
 #pragma unroll
         for (int w = 1; w < 4; ++w) {
-          const double* Tw = reinterpret_cast<const double*>(tw + 128 + 16 + w * WS);
+          const double* Tw = reinterpret_cast<const double*>(tw + 208 + w * WS);
           const double mw = Tw[NA * 4 * NT * 64 + lane];
           const double fw = exp_nonpos(mw - mm, etab);
           ssum = fma(Tw[(NA * 4 * NT + 1) * 64 + lane], fw, ssum);
@@ -1260,7 +1289,7 @@ __global__ __launch_bounds__(256, HM ? 1 : 2) void k_fft_wreg(long long B, long 
         const int sr = s0 + 4 * q;
 #pragma unroll
         for (int j = 0; j < 4; ++j) x[j] = T[sr * RS + g1 + 16 * j];
-        fft64_pass1<true>(x, lg2, g1, tw);
+        fft64_pass1<true, QCE_FFT_LANE_TW>(x, lg2, g1, QCE_FFT_LANE_TW ? tl : tw);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           if (OUT == 3)
@@ -1300,7 +1329,7 @@ struct FftChunkLds {
   static constexpr size_t tile = (size_t)TS * RS * 16;
   static constexpr size_t y2 = (size_t)N * TS * 8, e = (size_t)128 * TS * 8, sm = (size_t)2 * 4 * TS * 8;
   static constexpr size_t body = tile > y2 + e + sm ? tile : y2 + e + sm;
-  static constexpr size_t bytes = 128 * 16 + body + 32 * 8;  // + the exp table
+  static constexpr size_t bytes = 128 * 16 + body + 32 * 8 + 64 * 16;  // + the exp table, the pass-1 lane twiddles
 };
 
 template <int N, int OUT>
@@ -1324,6 +1353,7 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
   double2* E = reinterpret_cast<double2*>(reinterpret_cast<double*>(T) + N * TS);  // [CB * 2][4][16]
   double* SM = reinterpret_cast<double*>(E + CB * 2 * 64);         // [2][4][16] column maxima, column sums
   double* etab = reinterpret_cast<double*>(smem) + 2 * 128 + FftChunkLds<N>::body / 8;  // 2^(j/32), after the body
+  double2* tl = reinterpret_cast<double2*>(etab + 32);                                  // pass-1 lane twiddles (N = 256)
   const int tid = threadIdx.x;
   const long long b0 = (long long)blockIdx.x * TS;
   const int rows = (int)((B - b0) < TS ? (B - b0) : TS);
@@ -1349,13 +1379,14 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
         tw[t] = make_double2(cs, sn);
       }
       exp2_tab_init(etab, tid);
+      pass1_lane_tw(tl, 8, lg2, tid);
       __syncthreads();
       FW_STAMP(0);
       if (s1 >= rows) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) x[i] = make_double2(0.0, 0.0);
       }
-      fft256_pass1<false>(x, lg2, g, tw);
+      fft256_pass1<false, QCE_FFT_LANE_TW>(x, lg2, g, QCE_FFT_LANE_TW ? tl : tw);
 #pragma unroll
       for (int i = 0; i < 16; ++i) T[s1 * RS + g + 16 * i] = x[i];
     }
@@ -1565,7 +1596,7 @@ __global__ __launch_bounds__(256, 2) void k_fft_chunk(long long B, int lg1, int 
     double2 x[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) x[i] = T[s1 * RS + g + 16 * i];
-    fft256_pass1<true>(x, lg2, g, tw);
+    fft256_pass1<true, QCE_FFT_LANE_TW>(x, lg2, g, QCE_FFT_LANE_TW ? tl : tw);
     FW_STAMP(6);
     if (s1 < rows) {
       const long long o = (b0 + s1) * N + g;
@@ -1642,7 +1673,7 @@ struct FftChunkHmLds {
   static constexpr int TS = 16, RS = N + 1;
   static constexpr size_t tile = (size_t)TS * RS * 16;
   static constexpr size_t y2 = (size_t)N * TS * 8, e = (size_t)128 * TS * 8, sm = (size_t)2 * 4 * TS * 8;
-  static constexpr size_t bytes = 128 * 16 + tile + y2 + e + sm + 32 * 8;
+  static constexpr size_t bytes = 128 * 16 + tile + y2 + e + sm + 32 * 8 + 64 * 16;
 };
 
 template <int N, int OUT>
@@ -1665,6 +1696,7 @@ __global__ __launch_bounds__(256, 1) void k_fft_chunk_hm(long long B, int lg1, i
   double2* E = reinterpret_cast<double2*>(reinterpret_cast<char*>(Y2) + LD::y2);    // [CB * 2][4][16]
   double* SM = reinterpret_cast<double*>(reinterpret_cast<char*>(E) + LD::e);       // [2][4][16]
   double* etab = reinterpret_cast<double*>(reinterpret_cast<char*>(SM) + LD::sm);  // 2^(j/32)
+  double2* tl = reinterpret_cast<double2*>(etab + 32);                              // pass-1 lane twiddles (N = 256)
   const int tid = threadIdx.x;
   const long long b0 = (long long)blockIdx.x * TS;
   const int rows = (int)((B - b0) < TS ? (B - b0) : TS);
@@ -1688,12 +1720,13 @@ __global__ __launch_bounds__(256, 1) void k_fft_chunk_hm(long long B, int lg1, i
       tw[t] = make_double2(cs, sn);
     }
     exp2_tab_init(etab, tid);
+    pass1_lane_tw(tl, 8, lg2, tid);
     __syncthreads();
     if (s1 >= rows) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) x[i] = make_double2(0.0, 0.0);
     }
-    fft256_pass1<false>(x, lg2, g, tw);
+    fft256_pass1<false, QCE_FFT_LANE_TW>(x, lg2, g, QCE_FFT_LANE_TW ? tl : tw);
 #pragma unroll
     for (int i = 0; i < 16; ++i) T[s1 * RS + g + 16 * i] = x[i];
     __syncthreads();
@@ -1891,7 +1924,7 @@ __global__ __launch_bounds__(256, 1) void k_fft_chunk_hm(long long B, int lg1, i
     double2 x[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) x[i] = T[s1 * RS + g + 16 * i];
-    fft256_pass1<true>(x, lg2, g, tw);
+    fft256_pass1<true, QCE_FFT_LANE_TW>(x, lg2, g, QCE_FFT_LANE_TW ? tl : tw);
     if (s1 < rows) {
       const long long o = (b0 + s1) * N + g;
       if (OUT == 3) {
@@ -2063,7 +2096,7 @@ hipError_t launch_wave_c(const QceFftEstArgs& a, hipStream_t st) {
 
 template <int OUT, bool HM>
 hipError_t launch_wreg(const QceFftEstArgs& a, hipStream_t st) {
-  const size_t lds = 128 * 16 + 32 * 8 + (size_t)4 * (HM ? 1664 : 16 * 65) * 16;
+  const size_t lds = 128 * 16 + 32 * 8 + 64 * 16 + (size_t)4 * (HM ? 1664 : 16 * 65) * 16;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)k_fft_wreg<OUT, HM>, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -14,7 +14,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(config, launches, out_path):
+def child(config, launches, out_path, mean=False):
     sys.path.insert(0, ROOT)
     import torch
     from bench import CONFIGS, make_inputs
@@ -22,6 +22,7 @@ def child(config, launches, out_path):
     cfg = dict(CONFIGS[config])
     if cfg.pop("dense", False):
         os.environ["QCE_FFT"] = "0"
+    cfg["mean"] = mean  # as bench.py --mean
     means, covs, w, h, y, qz = make_inputs(cfg, 0)
     dev = torch.device("cuda", 0)
     st = torch.cuda.Stream(dev)
@@ -53,10 +54,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--child", default=None)
+    ap.add_argument("--mean", action="store_true", help="components with means (as bench.py --mean)")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     if a.child:
-        return child(a.config, a.launches, a.child)
+        return child(a.config, a.launches, a.child, a.mean)
     res = {}
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     for rnd in range(a.rounds):
@@ -65,7 +67,7 @@ def main():
             env = dict(os.environ, QCE_LIB=os.path.abspath(os.path.join(ROOT, lib)))
             outp = os.path.join(ROOT, "gpurun_out", f"ab_{name}.npy")
             p = subprocess.run([sys.executable, os.path.abspath(__file__), "--config", a.config, "--launches",
-                                str(a.launches), "--child", outp], env=env, capture_output=True, text=True,
+                                str(a.launches), "--child", outp] + (["--mean"] if a.mean else []), env=env, capture_output=True, text=True,
                                timeout=300)
             if p.returncode != 0:
                 print(json.dumps({"variant": name, "error": p.stderr[-2000:]}), flush=True)

@@ -8,7 +8,7 @@ Derived numbers (MI355X_MICROARCH.md):
   * MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x cycle base);
   * HBM-side traffic = 2 x FETCH_SIZE + WRITE_SIZE (gfx950 FETCH_SIZE counts half of a wide streaming read),
     per launch at the config's B; optional K=1 calibration passes check that factor on the kernel's y / h pattern.
-usage: pmc_report.py OUT KPAT CFG BUILD_ID
+usage: pmc_report.py OUT KPAT CFG BUILD_ID [TRAFFIC_NAME]   (default traffic_<CFG>; traffic_<CFG>_mean for --mean runs)
 """
 import csv
 import json
@@ -17,6 +17,7 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 base, pat, cfg, bid = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4]
+tname = sys.argv[5] if len(sys.argv) > 5 and sys.argv[5] else f"traffic_{cfg}"
 import bench  # noqa: E402
 
 C = bench.CONFIGS[cfg]
@@ -103,4 +104,4 @@ if f and w:
                "note": "hbm_bytes_per_launch: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, FETCH "
                        "doubled (gfx950), as MI355X_MICROARCH.md prescribes -- it counts L2 misses served by the "
                        "Infinity Cache too; dram: the requests that reached HBM; tools/pmc_kernel.sh + pmc_report.py"},
-              open(os.path.join(base, f"traffic_{cfg}.json"), "w"), indent=1)
+              open(os.path.join(base, f"{tname}.json"), "w"), indent=1)
