@@ -777,6 +777,14 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
   HIPCHK(m->means_y.ensure((size_t)K * M));
   HIPCHK(m->q0.ensure((size_t)K * M));
   HIPCHK(m->bvec.ensure((size_t)K * N));
+  if (m->has_mean) {
+    m->q0_zero = m->bvec_zero = nullptr;
+  } else if (m->q0_zero != m->q0.p || m->bvec_zero != m->bvec.p) {  // zero-mean: q0 = 0, b = 0 at every SNR
+    HIPCHK(hipMemsetAsync(m->q0.p, 0, sizeof(double2) * (size_t)K * M, st));
+    HIPCHK(hipMemsetAsync(m->bvec.p, 0, sizeof(double2) * (size_t)K * N, st));
+    m->q0_zero = m->q0.p;
+    m->bvec_zero = m->bvec.p;
+  }
   HIPCHK(m->gain.ensure((size_t)K * M));
   HIPCHK(m->cconst.ensure(K));
   HIPCHK(m->status.ensure(K));

@@ -31,6 +31,8 @@ struct DevBuf {
 struct qce_model {
   int K = 0, N = 0, device = 0;
   int a_identity_n = 0;   // m->A holds I_N (skips the upload + sync of a repeated A = NULL prepare)
+  const void* q0_zero = nullptr;    // zero-mean model: the q0 / bvec buffers at these addresses hold zeros
+  const void* bvec_zero = nullptr;  // (the prepare then skips their three launches)
   int packs_valid = 0;    // pack32 / pack64 built for the current prepare (lazy: 'all' mode never needs them)
   QcePrepareArgs pack_args{};
   int beta_first = 0;  // QCE_OPT_BETA_FIRST: multi-bit Cr mixes with the first gain (blmmse.py:53, :86)

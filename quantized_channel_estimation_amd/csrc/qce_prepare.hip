@@ -840,14 +840,19 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
   if ((e = zgemm(0, 0, N, M, M, one, p.V, M, (long long)N * M, p.Linv, M, (long long)M * M, zero, p.W, M,
                  (long long)N * M, K, st)) != hipSuccess)
     return e;
-  // q0 = Linv mu_y (M x 1);  b = mu - V q0 (N x 1)
-  if ((e = zgemm(0, 0, M, 1, M, one, p.Linv, M, (long long)M * M, p.means_y, 1, M, zero, p.q0, 1, M, K, st)) !=
-      hipSuccess)
-    return e;
-  if ((e = hipMemcpyAsync(p.bvec, p.means, sizeof(double2) * (size_t)K * N, hipMemcpyDeviceToDevice, st)) != hipSuccess)
-    return e;
-  if ((e = zgemm(0, 0, N, 1, M, mone, p.V, M, (long long)N * M, p.q0, 1, M, one, p.bvec, 1, N, K, st)) != hipSuccess)
-    return e;
+  // q0 = Linv mu_y (M x 1);  b = mu - V q0 (N x 1).  Zero-mean models: both are zero for every SNR -- the C-ABI
+  // layer zero-fills them once per buffer (qce_capi.hip prepare) and the three launches are skipped
+  if (p.has_mean) {
+    if ((e = zgemm(0, 0, M, 1, M, one, p.Linv, M, (long long)M * M, p.means_y, 1, M, zero, p.q0, 1, M, K, st)) !=
+        hipSuccess)
+      return e;
+    if ((e = hipMemcpyAsync(p.bvec, p.means, sizeof(double2) * (size_t)K * N, hipMemcpyDeviceToDevice, st)) !=
+        hipSuccess)
+      return e;
+    if ((e = zgemm(0, 0, N, 1, M, mone, p.V, M, (long long)N * M, p.q0, 1, M, one, p.bvec, 1, N, K, st)) !=
+        hipSuccess)
+      return e;
+  }
   return qce_launch_pack_selective(p, st);
 }
 
