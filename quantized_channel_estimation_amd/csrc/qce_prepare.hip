@@ -468,6 +468,125 @@ __global__ __launch_bounds__(NT) void k_chol_inv_lds(int M, const double2* __res
   }
 }
 
+// k_chol_inv_lds with two columns per barrier phase (M / 2 barriers instead of M; the phases are latency-bound,
+// so the halved count is what shortens the kernel).  Phase (j, j + 1) reads the state before step j and applies
+// both steps at once, with step j's updates of column j + 1 and row j + 1 (the operands of step j + 1) formed on the
+// fly by every thread that needs them:
+//   b_r   = a_r,j+1 - a_rj conj(a_j+1,j) / a_jj            (r > j: column j + 1 after step j; d1 = b_j+1)
+//   a_rc -= a_rj conj(a_cj) / a_jj,  then -= b_r conj(b_c) / d1          (r >= c >= j + 2)
+//   x'_c  = x_j+1,c - (a_j+1,j / a_jj) x_jc                 (c <= j + 1; x'_j+1 = 1)
+//   x_ic -= (a_ij / a_jj) x_jc,  then -= (b_i / d1) x'_c                  (i >= j + 2, c <= j + 1)
+// Column j + 1 and row j + 1 themselves take their step-j values in the NEXT phase (no thread reads them there), or
+// after the loop for the last pair; the operations and their order per entry are those of the one-column kernel.
+template <int NT>
+__global__ __launch_bounds__(NT) void k_chol_inv_lds2(int M, const double2* __restrict__ Cr,
+                                                       double2* __restrict__ Linv, const double* __restrict__ logw,
+                                                       double* __restrict__ cconst, int* __restrict__ status) {
+  constexpr int LD = 65;
+  __shared__ double2 a[64 * LD];
+  __shared__ double2 x[64 * LD];
+  __shared__ double piv[64];
+  __shared__ unsigned short tri_rc[63 * 64 / 2];
+  const int k = blockIdx.x, tid = threadIdx.x;
+  const double2* src = Cr + (long long)k * M * M;
+  for (int e = tid; e < M * M; e += NT) {
+    const int r = e / M, c = e % M;
+    a[r * LD + c] = src[e];
+    x[r * LD + c] = make_double2(r == c ? 1.0 : 0.0, 0.0);
+  }
+  for (int rr = tid >> 6; rr < 63; rr += NT / 64)
+    for (int cc = tid & 63; cc <= rr; cc += 64) tri_rc[rr * (rr + 1) / 2 + cc] = (unsigned short)((rr << 8) | cc);
+  __syncthreads();
+  // step q's own updates of column q + 1 (factor) and row q + 1 (inverse), deferred from the phase of pair (q, q + 1)
+  auto settle = [&](int q) {
+    const double inv0 = 1.0 / a[q * LD + q].x;
+    const double2 aq1q = a[(q + 1) * LD + q];
+    const int ncol = M - q - 1;
+    for (int t = tid; t < ncol + q + 1; t += NT) {
+      if (t < ncol) {
+        const int r = q + 1 + t;
+        const double2 pr = cmulc(a[r * LD + q], aq1q);
+        a[r * LD + q + 1] = csub(a[r * LD + q + 1], make_double2(pr.x * inv0, pr.y * inv0));
+      } else {
+        const int c = t - ncol;
+        x[(q + 1) * LD + c] = csub(x[(q + 1) * LD + c], cmul(make_double2(aq1q.x * inv0, aq1q.y * inv0), x[q * LD + c]));
+      }
+    }
+  };
+  bool bad = false;
+  int j = 0;
+  for (; j + 1 < M; j += 2) {
+    const double ajj = a[j * LD + j].x;  // final: updated by the previous phase before the barrier
+    if (!(ajj > 0.0)) {                  // same value in every thread: uniform exit
+      bad = true;
+      break;
+    }
+    const double inv0 = 1.0 / ajj;
+    const double2 aj1j = a[(j + 1) * LD + j];
+    const double2 pjj = cmulc(aj1j, aj1j);
+    const double d1 = a[(j + 1) * LD + j + 1].x - pjj.x * inv0;
+    if (!(d1 > 0.0)) {
+      bad = true;
+      break;
+    }
+    const double inv1 = 1.0 / d1;
+    const double2 lj1 = make_double2(aj1j.x * inv0, aj1j.y * inv0);
+    if (j >= 2) settle(j - 2);
+    const int n = M - j - 2;
+    const int tri = n * (n + 1) / 2;
+    for (int t = tid; t < tri; t += NT) {
+      const unsigned v = tri_rc[t];
+      const int r = j + 2 + (int)(v >> 8), c = j + 2 + (int)(v & 255u);
+      const double2 arj = a[r * LD + j], acj = a[c * LD + j];
+      const double2 qr = cmulc(arj, aj1j), qc = cmulc(acj, aj1j);
+      const double2 br = csub(a[r * LD + j + 1], make_double2(qr.x * inv0, qr.y * inv0));
+      const double2 bc = csub(a[c * LD + j + 1], make_double2(qc.x * inv0, qc.y * inv0));
+      const double2 p0 = cmulc(arj, acj), p1 = cmulc(br, bc);
+      double2 v2 = csub(a[r * LD + c], make_double2(p0.x * inv0, p0.y * inv0));
+      a[r * LD + c] = csub(v2, make_double2(p1.x * inv1, p1.y * inv1));
+    }
+    const int nr = M - j - 2, nc = j + 2;
+    const float rnc = 1.0f / (float)nc;  // t / nc through an fp32 reciprocal and one correction (t < 4096)
+    for (int t = tid; t < nr * nc; t += NT) {
+      int q = (int)((float)t * rnc);
+      q += (q + 1) * nc <= t ? 1 : 0;
+      q -= q * nc > t ? 1 : 0;
+      const int i = j + 2 + q, c = t - q * nc;
+      const double2 aij = a[i * LD + j];
+      const double2 qi = cmulc(aij, aj1j);
+      const double2 bi = csub(a[i * LD + j + 1], make_double2(qi.x * inv0, qi.y * inv0));
+      const double2 xj = x[j * LD + c];
+      const double2 xj1 = csub(x[(j + 1) * LD + c], cmul(lj1, xj));
+      double2 v2 = csub(x[i * LD + c], cmul(make_double2(aij.x * inv0, aij.y * inv0), xj));
+      x[i * LD + c] = csub(v2, cmul(make_double2(bi.x * inv1, bi.y * inv1), xj1));
+    }
+    __syncthreads();
+  }
+  if (!bad && j >= 2) {  // the last pair's column / row
+    settle(j - 2);
+    __syncthreads();
+  }
+  if (!bad && j < M && !(a[j * LD + j].x > 0.0)) bad = true;  // odd M: the last column
+  if (bad) {
+    if (tid == 0) status[k] = 1;
+    return;
+  }
+  for (int i = tid; i < M; i += NT) piv[i] = sqrt(a[i * LD + i].x);
+  __syncthreads();
+  double2* dst = Linv + (long long)k * M * M;
+  for (int e = tid; e < M * M; e += NT) {
+    const int r = e / M, c = e % M;
+    const double2 v = x[r * LD + c];
+    dst[e] = make_double2(v.x / piv[r], v.y / piv[r]);
+  }
+  if (tid == 0) {
+    double ld = 0.0;
+    for (int i = 0; i < M; ++i) ld += log(1.0 / piv[i]);
+    cconst[k] = -(M * log(3.14159265358979323846)) + 2.0 * ld + logw[k];
+    status[k] = 0;
+  }
+}
+
 // Cholesky Cr_k = L L^H and L^{-1} for M <= 64 by ONE wave per component (lane r owns row r; the matrix in LDS
 // with a padded row stride, 66.5 KB), wave-synchronous: no multi-wave barriers in the 2M sequential steps, which
 // is what bounds a per-component factorisation (the K components run side by side, two per CU).
@@ -803,7 +922,18 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
       const int v = e ? atoi(e) : 1024;
       return (v == 256 || v == 512 || v == 1024) ? v : 1024;
     }();
-    if (nt == 1024)
+    // two columns per barrier phase from M = 16 (tools/chol_pairs_check.py, whole prepare: metric 0.138 -> 0.131 ms,
+    // cfg2 0.126 -> 0.121 ms, tables within 8e-16); QCE_CHOL_PAIRS=0: one column per phase (A/B)
+    static const bool pairs_env = [] {
+      const char* e = getenv("QCE_CHOL_PAIRS");
+      return !(e && e[0] == '0');
+    }();
+    const bool pairs = pairs_env && M >= 16;
+    if (pairs && nt == 1024)
+      hipLaunchKernelGGL(k_chol_inv_lds2<1024>, dim3(K), dim3(1024), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
+    else if (pairs && nt == 512)
+      hipLaunchKernelGGL(k_chol_inv_lds2<512>, dim3(K), dim3(512), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
+    else if (nt == 1024)
       hipLaunchKernelGGL(k_chol_inv_lds<1024>, dim3(K), dim3(1024), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
     else if (nt == 512)
       hipLaunchKernelGGL(k_chol_inv_lds<512>, dim3(K), dim3(512), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
