@@ -1,4 +1,5 @@
-"""Segment cycle breakdown of k_est_all_f64 at a bench configuration (default metric; argv[1]: cfg4, ...), diagnostic build.
+"""Segment cycle breakdown of k_est_all_f64 at a bench configuration (default metric; argv[1]: cfg4, ...; argv[2]: K),
+diagnostic build.
 
   python -m quantized_channel_estimation_amd.build --stamps      # libqce_stamps.so
   QCE_LIB=quantized_channel_estimation_amd/libqce_stamps.so python tools/f64_stamps.py
@@ -19,6 +20,8 @@ def main():
     from quantized_channel_estimation_amd import _lib
     import bench
     cfg = dict(bench.CONFIGS[sys.argv[1] if len(sys.argv) > 1 else "metric"])
+    if len(sys.argv) > 2:  # argv[2]: components (a K-shard rank's share, e.g. 16 of the metric's 128)
+        cfg["K"] = int(sys.argv[2])
     means, covs, w, h, y, qz = bench.make_inputs(cfg, 0)
     dm = _lib.DeviceModel(means, covs, w)
     dm.prepare(None, cfg["snr"], 1.0)
