@@ -780,10 +780,14 @@ def main():
         }
         line.update(extras)
         print(json.dumps(line), flush=True)
-    if kshard and native:  # tear the communicator down while every rank is still here
-        torch.cuda.synchronize(dev)
-        shard.native.close()
-        comm.close()
+    # explicit teardown while every rank and the runtimes are still here (not left to exit-time destructors)
+    torch.cuda.synchronize(dev)
+    if kshard:
+        shard.close()
+        if native:
+            comm.close()
+    else:
+        model.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

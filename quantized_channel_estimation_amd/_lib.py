@@ -3,8 +3,11 @@
 The library is the only compute path: if it is missing or no HIP device is visible, every
 estimator call raises — there is no CPU fallback in this package.
 """
+import atexit
 import ctypes
 import os
+import threading
+import weakref
 
 import numpy as np
 
@@ -152,6 +155,26 @@ def check(rc):
     raise QceError(f"[qce status {rc}] {msg}")
 
 
+# Every live handle of this process (DeviceModel, Comm, KShard), closed in dependency order by an atexit hook while the
+# HIP runtime and RCCL are still fully up: objects Python never collects (reference cycles, module
+# globals) otherwise reach their teardown only through the runtimes' own exit-time destructors.
+_live = {"kshard": weakref.WeakSet(), "comm": weakref.WeakSet(), "model": weakref.WeakSet()}
+
+
+def _close_all_at_exit():
+    if os.environ.get("QCE_NO_EXIT_CLOSE") == "1":  # diagnostic: leave teardown to the runtimes' destructors
+        return
+    for kind in ("kshard", "model", "comm"):
+        for obj in list(_live[kind]):
+            try:
+                obj.close()
+            except Exception:
+                pass
+
+
+atexit.register(_close_all_at_exit)
+
+
 def build_id():
     """Source digest the loaded libqce.so was built from (qce_build_id)."""
     return load().qce_build_id().decode()
@@ -202,31 +225,43 @@ class _PinnedBlock:
 class _PinnedPool:
     """Free page-locked blocks kept for reuse (the drop-in numpy API's result arrays): the estimate's D2H lands in
     them directly, and a block the caller dropped serves the next call without new page faults.  At most
-    `cap_bytes` of free blocks are kept; the rest are freed."""
+    `cap_bytes` of free blocks are kept; the rest are freed.  Thread-safe: an array dropped on another
+    thread returns its block while take() searches, so the search and the removal are one critical section and the
+    block handed out is checked against the request."""
 
     def __init__(self, cap_bytes=1 << 30):
         self.cap = cap_bytes
-        self.free = []  # _PinnedBlock-like records (ptr, nbytes) not referenced by any array
+        self.free = []  # (ptr, nbytes) records of blocks not referenced by any array
+        self.lock = threading.Lock()
 
     def take(self, nbytes):
-        best = None
-        for i, (p, n) in enumerate(self.free):
-            if n >= nbytes and n <= 2 * nbytes and (best is None or n < self.free[best][1]):
-                best = i
+        nbytes = int(nbytes)
+        with self.lock:
+            best = None
+            for rec in self.free:
+                if nbytes <= rec[1] <= 2 * nbytes and (best is None or rec[1] < best[1]):
+                    best = rec
+            if best is not None:
+                self.free.remove(best)  # by identity of the record, inside the lock
         if best is not None:
-            p, n = self.free.pop(best)
+            p, n = best
+            if n < nbytes:  # pragma: no cover - guarded above; never hand out a block the D2H would overrun
+                raise QceError(f"pinned pool block of {n} bytes for a request of {nbytes}")
             blk = _PinnedBlock.__new__(_PinnedBlock)
             blk.ptr, blk.nbytes = p, n
             return blk
         return _PinnedBlock(nbytes)
 
     def give_back(self, blk):
-        if blk.ptr is None:
-            return
-        self.free.append((blk.ptr, blk.nbytes))
-        blk.ptr = None
-        while sum(n for _, n in self.free) > self.cap:
-            p, _ = self.free.pop(0)
+        to_free = []
+        with self.lock:
+            if blk.ptr is None:
+                return
+            self.free.append((blk.ptr, blk.nbytes))
+            blk.ptr = None
+            while sum(n for _, n in self.free) > self.cap:
+                to_free.append(self.free.pop(0)[0])
+        for p in to_free:
             load().qce_host_free(p)
 
 
@@ -266,6 +301,7 @@ class DeviceModel:
         h = _vp()
         check(lib.qce_model_create(K, N, ptr(means), ptr(covs), ptr(w), int(device), ctypes.byref(h)))
         self._h = h
+        _live["model"].add(self)
         self.K, self.N, self.device = K, N, int(device)
         self.M = 0
         self.precision = "f64"
@@ -291,6 +327,7 @@ class DeviceModel:
         if getattr(self, "_h", None):
             load().qce_model_destroy(self._h)
             self._h = None
+            _live["model"].discard(self)
 
     def __del__(self):
         try:
@@ -507,6 +544,22 @@ def kshard_slice(K, world, rank):
     return lo.value, hi.value
 
 
+def kshard_layout(world, rank):
+    """(world, rank) a K-shard's rows are laid out for: the communicator's, or on a world-1 communicator the test hook
+    QCE_KSHARD_EMULATE_WORLD="W[:R]" (one GPU rehearsing rank R of a W-GPU step; csrc/qce_kshard.hip)."""
+    e = os.environ.get("QCE_KSHARD_EMULATE_WORLD", "")
+    if world != 1 or not e:
+        return world, rank
+    try:
+        w, _, r = e.partition(":")
+        w, r = int(w), int(r or 0)
+    except ValueError:
+        return world, rank
+    if w < 2 or w > 4096 or not 0 <= r < w:
+        return world, rank
+    return w, r
+
+
 def kshard_rows(B, chunks, world, rank, scatter):
     """Global row ranges [(r0, r1), ...] of the rows a rank's qce_kshard_estimate writes, in h_out order."""
     cap = max(1, int(chunks)) + 1
@@ -536,6 +589,7 @@ class Comm:
         check(load().qce_comm_init(ctypes.cast(buf, _vp), int(rank), int(world), int(device), ctypes.byref(h)))
         self._h, self._cb = h, None
         self.rank, self.world, self.device, self.kind = int(rank), int(world), int(device), COMM_RCCL
+        _live["comm"].add(self)
 
     @classmethod
     def host(cls, rank, world, device, fn):
@@ -559,6 +613,7 @@ class Comm:
                                         ctypes.byref(h)))
         self._h = h
         self.rank, self.world, self.device, self.kind = int(rank), world, int(device), COMM_HOST
+        _live["comm"].add(self)
         return self
 
     @property
@@ -569,6 +624,7 @@ class Comm:
         if getattr(self, "_h", None):
             load().qce_comm_destroy(self._h)
             self._h = None
+            _live["comm"].discard(self)
 
     def __del__(self):
         try:
@@ -586,6 +642,8 @@ class KShard:
         check(load().qce_kshard_create(model.handle, comm.handle, int(K_total), ctypes.byref(h)))
         self._h, self.model, self.comm, self.K = h, model, comm, int(K_total)
         self._keep = None
+        self.layout_world, self.layout_rank = kshard_layout(comm.world, comm.rank)
+        _live["kshard"].add(self)
 
     def set_spare(self, spare):
         """Double-buffered tables: `spare` another DeviceModel of the same shard (qce_kshard_set_spare)."""
@@ -596,6 +654,8 @@ class KShard:
         if getattr(self, "_h", None):
             load().qce_kshard_destroy(self._h)
             self._h = None
+            self._keep = None
+            _live["kshard"].discard(self)
 
     def __del__(self):
         try:
@@ -624,11 +684,15 @@ class KShard:
 
     def estimate(self, y, mode=MODE_ALL, param=0.0, chunks=2, scatter=True, out=None, stream=None):
         """y (B, M) complex128 CUDA tensor (the same on every rank) -> (rows, h): h the estimates of the global rows
-        `rows` (a list of (r0, r1) ranges in h's row order).  Asynchronous on `stream`; finish() is the sync point."""
+        `rows` (a list of (r0, r1) ranges in h's row order).  Asynchronous on `stream` (default: torch's current
+        stream of y's device); finish() is the sync point."""
         import torch
         B = y.shape[0]
+        cur = torch.cuda.current_stream(y.device)
+        if stream is None:
+            stream = cur.cuda_stream
         ch = int(chunks) if mode == MODE_ALL else 1
-        rows = kshard_rows(B, ch, self.comm.world, self.comm.rank, scatter)
+        rows = kshard_rows(B, ch, self.layout_world, self.layout_rank, scatter)
         n = sum(b - a for a, b in rows)
         if out is None:
             out = torch.empty((n, self.model.N), dtype=torch.complex128, device=y.device)
@@ -640,8 +704,18 @@ class KShard:
                                          ptr(out), stream))
         # y and h of the steps whose collectives / row finalisation may still run on the library's communication
         # stream stay alive: the last two (step t+2 waits on the compute stream for step t's communication-stream work,
-        # qce_kshard_estimate), so memory does not grow with the number of steps between finish() calls
-        self._keep = ((self._keep or []) + [(y, out)])[-2:]
+        # qce_kshard_estimate), so memory does not grow with the number of steps between finish() calls.  The step
+        # dropped here is safe for torch's allocator to reuse only on a stream ordered behind that wait: torch's current
+        # stream when the step ran on it; otherwise the tensors are recorded on the step's stream, whose
+        # work now includes the wait, so the allocator holds them until it has passed.
+        keep = (self._keep or []) + [(y, out, int(stream))]
+        if len(keep) > 2:
+            for yy, oo, s in keep[:-2]:
+                if s != cur.cuda_stream:
+                    ext = torch.cuda.ExternalStream(s, device=y.device)
+                    yy.record_stream(ext)
+                    oo.record_stream(ext)
+        self._keep = keep[-2:]
         return rows, out
 
     def finish(self, stream=None):

@@ -133,10 +133,10 @@ bool want_f64(const qce_model* m) {
 // (m, s, acc) partial when h == nullptr (K-shard path)
 int run_f64(qce_model* m, const double2* dy, long long B, double2* h, double* om, double* os, double* oa,
             hipStream_t st, double* pk = nullptr, const double* shift = nullptr) {
-  const long long TS = m->f64_g3 ? 16LL * qce_f64g_waves() : qce_f64_tile(m->MP, m->NP);
+  const long long TS = m->f64_g3 == 2 ? 64LL : (m->f64_g3 ? 16LL * qce_f64g_waves() : qce_f64_tile(m->MP, m->NP));
   const long long tiles = (B + TS - 1) / TS;
-  // one 8-wave workgroup per CU (its ring fills the LDS), or two 4-wave ones (3M kernel built with 4 waves)
-  long long slots = (long long)m->sched_cus() * (m->f64_g3 ? 8 / qce_f64g_waves() : 1);
+  // one 8-wave workgroup per CU (its ring / y tile fills the LDS), or two 4-wave ones (3M kernel built with 4 waves)
+  long long slots = (long long)m->sched_cus() * (m->f64_g3 == 1 ? 8 / qce_f64g_waves() : 1);
   const char* e = getenv("QCE_WORKGROUPS");
   if (e && atoll(e) > 0) slots = atoll(e);
   long long nwg, R, L;
@@ -778,12 +778,13 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
   HIPCHK(m->q0.ensure((size_t)K * M));
   HIPCHK(m->bvec.ensure((size_t)K * N));
   if (m->has_mean) {
-    m->q0_zero = m->bvec_zero = nullptr;
-  } else if (m->q0_zero != m->q0.p || m->bvec_zero != m->bvec.p) {  // zero-mean: q0 = 0, b = 0 at every SNR
-    HIPCHK(hipMemsetAsync(m->q0.p, 0, sizeof(double2) * (size_t)K * M, st));
-    HIPCHK(hipMemsetAsync(m->bvec.p, 0, sizeof(double2) * (size_t)K * N, st));
-    m->q0_zero = m->q0.p;
-    m->bvec_zero = m->bvec.p;
+    m->q0_zeroed = m->bvec_zeroed = 0;  // the prepare writes them
+  } else if (m->q0_zeroed < (size_t)K * M || m->bvec_zeroed < (size_t)K * N) {  // zero-mean: q0 = 0, b = 0 at every SNR
+    m->q0_zeroed = m->bvec_zeroed = 0;
+    HIPCHK(hipMemsetAsync(m->q0.p, 0, sizeof(double2) * m->q0.n, st));
+    HIPCHK(hipMemsetAsync(m->bvec.p, 0, sizeof(double2) * m->bvec.n, st));
+    m->q0_zeroed = m->q0.n;
+    m->bvec_zeroed = m->bvec.n;
   }
   HIPCHK(m->gain.ensure((size_t)K * M));
   HIPCHK(m->cconst.ensure(K));
@@ -888,8 +889,12 @@ static int prepare_impl(qce_model* m, const double* A, int M, double snr_db, dou
                                 reinterpret_cast<double*>(m->pack_ws.p), st));
   } else if (m->f64_active) {
     // FP64 tables of the fused kernel (reference precision): 3M layout where the 3M kernel covers the shape
-    m->f64_g3 = qce_f64g_shape(MP, NP) ? 1 : 0;
-    if (m->f64_g3) {
+    m->f64_g3 = qce_f64g_shape(MP, NP) ? 1 : (qce_f64h_shape(MP, NP) ? 2 : 0);
+    if (m->f64_g3 == 2) {
+      HIPCHK(m->pack_f64.ensure((size_t)qce_pack_f64h_bytes(m->has_mean) * K));
+      HIPCHK(qce_launch_pack_f64h(K, M, N, m->has_mean, m->Linv.p, m->W.p, m->q0.p, m->bvec.p,
+                                  reinterpret_cast<double*>(m->pack_f64.p), st));
+    } else if (m->f64_g3) {
       HIPCHK(m->pack_f64.ensure((size_t)qce_pack_f64g_bytes(MP, NP, m->has_mean) * K));
       HIPCHK(qce_launch_pack_f64g(K, M, N, MP, NP, m->has_mean, m->Linv.p, m->W.p, m->q0.p, m->bvec.p,
                                   reinterpret_cast<double*>(m->pack_f64.p), st));
@@ -1044,6 +1049,20 @@ int qce_host_free(void* p) {
   return QCE_OK;
 }
 
+namespace {
+// Every return of a host-I/O pipeline, the error paths included, first waits for its copy streams: the
+// caller's arrays are unregistered (HostDma) or handed back right after, and an async copy may still be using them.
+struct CopyStreamsDrain {
+  hipStream_t a, b;
+  ~CopyStreamsDrain() {
+    if (a) (void)hipStreamSynchronize(a);
+    if (b) (void)hipStreamSynchronize(b);
+  }
+};
+// estimate_host_direct could not get its whole-batch device scratch: the bounded staged pipeline takes the batch
+constexpr int kDirectNoScratch = -1;
+}  // namespace
+
 // Host numpy I/O straight from / into the caller's arrays (both DMA-able, see HostDma): per chunk H2D on a copy
 // stream, the estimate on the compute stream, D2H on a second copy stream -- no host copies, one sync at the end.
 static int estimate_host_direct(qce_model* m, const double* y, long long B, int mode, double mode_param,
@@ -1056,8 +1075,13 @@ static int estimate_host_direct(qce_model* m, const double* y, long long B, int 
     if (!hp.ev_in[i]) HIPCHK(hipEventCreateWithFlags(&hp.ev_in[i], hipEventDisableTiming));
     if (!hp.ev_c[i]) HIPCHK(hipEventCreateWithFlags(&hp.ev_c[i], hipEventDisableTiming));
   }
-  HIPCHK(m->y_scr.ensure((size_t)B * M));
-  HIPCHK(m->h_scr.ensure((size_t)B * N));
+  if (m->y_scr.ensure((size_t)B * M) != hipSuccess || m->h_scr.ensure((size_t)B * N) != hipSuccess) {
+    (void)hipGetLastError();
+    m->y_scr.release();  // the staged pipeline sizes its own (bounded) scratch
+    m->h_scr.release();
+    return kDirectNoScratch;
+  }
+  CopyStreamsDrain drain{hp.s_in, hp.s_out};
   const std::vector<long long> bd = direct_chunks(B);
   const double2* ys = reinterpret_cast<const double2*>(y);
   double2* hs = reinterpret_cast<double2*>(h_out);
@@ -1100,6 +1124,7 @@ static int estimate_host_pipelined(qce_model* m, const double* y, long long B, l
     if (!hp.ev_c[i]) HIPCHK(hipEventCreateWithFlags(&hp.ev_c[i], hipEventDisableTiming));
     if (!hp.ev_out[i]) HIPCHK(hipEventCreateWithFlags(&hp.ev_out[i], hipEventDisableTiming));
   }
+  CopyStreamsDrain drain{hp.s_in, hp.s_out};
   if (hp.cap_y < (size_t)C * M || hp.cap_h < (size_t)C * N) {
     HIPCHK(hipStreamSynchronize(hp.s_in));
     HIPCHK(hipStreamSynchronize(hp.s_out));
@@ -1116,28 +1141,35 @@ static int estimate_host_pipelined(qce_model* m, const double* y, long long B, l
     hp.cap_y = (size_t)C * M;
     hp.cap_h = (size_t)C * N;
   }
-  HIPCHK(m->y_scr.ensure((size_t)B * M));
-  HIPCHK(m->h_scr.ensure((size_t)B * N));
+  // two device slots per direction, like the pinned ones (bounded scratch: a batch of any size streams through)
+  HIPCHK(m->y_scr.ensure((size_t)2 * C * M));
+  HIPCHK(m->h_scr.ensure((size_t)2 * C * N));
   const long long nc = (B + C - 1) / C;
   const double2* ys = reinterpret_cast<const double2*>(y);
   double2* hs = reinterpret_cast<double2*>(h_out);
+  // the copy-in stream starts behind the compute stream's earlier work (the scratch slots' previous readers)
+  HIPCHK(hipEventRecord(hp.ev_c[0], st));
+  HIPCHK(hipStreamWaitEvent(hp.s_in, hp.ev_c[0], 0));
   int rc = QCE_OK;
   for (long long i = 0; i <= nc; ++i) {
     if (i < nc && rc == QCE_OK) {
       const int s = (int)(i & 1);
       const long long o = i * C, n = (B - o) < C ? (B - o) : C;
+      double2* yslot = m->y_scr.p + (size_t)s * C * M;
+      double2* hslot = m->h_scr.p + (size_t)s * C * N;
       if (i >= 2) HIPCHK(hipEventSynchronize(hp.ev_in[s]));  // slot s: chunk i-2's upload has read it
       par_memcpy(hp.pin_y[s], ys + o * M, sizeof(double2) * (size_t)n * M);
-      HIPCHK(hipMemcpyAsync(m->y_scr.p + o * M, hp.pin_y[s], sizeof(double2) * (size_t)n * M, hipMemcpyHostToDevice,
-                            hp.s_in));
+      if (i >= 2) HIPCHK(hipStreamWaitEvent(hp.s_in, hp.ev_c[s], 0));  // chunk i-2's estimate has read y slot s
+      HIPCHK(hipMemcpyAsync(yslot, hp.pin_y[s], sizeof(double2) * (size_t)n * M, hipMemcpyHostToDevice, hp.s_in));
       HIPCHK(hipEventRecord(hp.ev_in[s], hp.s_in));
       HIPCHK(hipStreamWaitEvent(st, hp.ev_in[s], 0));
-      rc = qce_estimate(m, reinterpret_cast<const double*>(m->y_scr.p + o * M), n, mode, mode_param,
-                        reinterpret_cast<double*>(m->h_scr.p + o * N), QCE_IO_DEVICE, st);
+      if (i >= 2) HIPCHK(hipStreamWaitEvent(st, hp.ev_out[s], 0));  // chunk i-2's download has read h slot s
+      rc = qce_estimate(m, reinterpret_cast<const double*>(yslot), n, mode, mode_param,
+                        reinterpret_cast<double*>(hslot), QCE_IO_DEVICE, st);
       if (rc == QCE_OK) {
         HIPCHK(hipEventRecord(hp.ev_c[s], st));
         HIPCHK(hipStreamWaitEvent(hp.s_out, hp.ev_c[s], 0));
-        HIPCHK(hipMemcpyAsync(hp.pin_h[s], m->h_scr.p + o * N, sizeof(double2) * (size_t)n * N, hipMemcpyDeviceToHost,
+        HIPCHK(hipMemcpyAsync(hp.pin_h[s], hslot, sizeof(double2) * (size_t)n * N, hipMemcpyDeviceToHost,
                               hp.s_out));
         HIPCHK(hipEventRecord(hp.ev_out[s], hp.s_out));
       }
@@ -1174,7 +1206,10 @@ int qce_estimate(qce_model* m, const double* y, int64_t B, int mode, double mode
       if (!(de && de[0] == '0')) {
         HostDma dy(const_cast<double*>(y), sizeof(double2) * (size_t)B * m->M);
         HostDma dh(h_out, sizeof(double2) * (size_t)B * m->N);
-        if (dy.ok && dh.ok) return estimate_host_direct(m, y, B, mode, mode_param, h_out, st);
+        if (dy.ok && dh.ok) {
+          const int drc = estimate_host_direct(m, y, B, mode, mode_param, h_out, st);
+          if (drc != kDirectNoScratch) return drc;
+        }
       }
       return estimate_host_pipelined(m, y, B, C, mode, mode_param, h_out, st);
     }
@@ -1795,6 +1830,7 @@ int qce_model_set_option(qce_model* m, int option, double value) {
   if (option == QCE_OPT_RESERVE_CUS) {
     if (value < 0.0 || value != floor(value)) return fail(QCE_EARG, "reserve_cus must be an integer >= 0");
     m->reserve_cus = value > 1e6 ? 1000000 : (int)value;
+    m->reserve_set = 1;
     return QCE_OK;
   }
   if (option == QCE_OPT_PRECISION) {

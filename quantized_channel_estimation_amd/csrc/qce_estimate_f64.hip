@@ -253,7 +253,9 @@ hipError_t qce_f64g_launch_mp(const QceF64Args& a, bool out_partial, hipStream_t
 
 hipError_t qce_launch_est_f64(const QceF64Args& a, bool out_partial, hipStream_t st) {
   hipError_t e;
-  if (a.g3) {
+  if (a.g3 == 2) {
+    e = qce_f64h_launch(a, out_partial, st);
+  } else if (a.g3) {
     switch (a.MP) {
       case 16: e = qce_f64g_launch_mp<16>(a, out_partial, st); break;
       case 32: e = qce_f64g_launch_mp<32>(a, out_partial, st); break;
@@ -268,7 +270,7 @@ hipError_t qce_launch_est_f64(const QceF64Args& a, bool out_partial, hipStream_t
     default: e = hipErrorInvalidValue;
   }
   if (e != hipSuccess) return e;
-  const long long TS = a.g3 ? 16LL * QCE_F64G_NW : qce_f64_tile(a.MP, a.NP);
+  const long long TS = a.g3 == 2 ? 64LL : (a.g3 ? 16LL * QCE_F64G_NW : qce_f64_tile(a.MP, a.NP));
   const long long tiles = (a.B + TS - 1) / TS;
   const long long tail0 = (long long)a.R * a.nwg;
   if (a.L > 0 && tiles > tail0) {  // some tail tile may be cut between workgroups

@@ -103,8 +103,15 @@ struct QceF64Args {
   const double* shift = nullptr;  // device pointer: the shared shift M* of the packed partial
   unsigned long long* stamps = nullptr;  // diagnostic builds (-DQCE_STAMPS): per-wave segment cycles
   int waves = 8;  // workgroup shape where M, N <= 64: 8 waves x 1 column tile (two per SIMD), or 4 x 2 (QCE_F64_WAVES=4)
-  int g3 = 0;     // 3M tables / kernel (k_est_all_f64g, padded M, N <= 64; always 8 waves x 16 samples)
+  int g3 = 0;     // 3M tables / kernel: 1 k_est_all_f64g (padded M, N <= 64; 8 waves x 16 samples), 2 k_est_all_f64h
+                 // (padded M = N = 128: row halves, y in LDS; 8 waves x 64 samples)
 };
+// k_est_all_f64h (qce_f64h.hip): the 3M kernel for padded M = N = 128
+bool qce_f64h_shape(int MP, int NP);
+long long qce_pack_f64h_bytes(int has_mean);
+hipError_t qce_launch_pack_f64h(int K, int M, int N, int has_mean, const double2* Linv, const double2* W,
+                                const double2* q0, const double2* bvec, double* pack, hipStream_t st);
+hipError_t qce_f64h_launch(const QceF64Args& a, bool out_partial, hipStream_t st);
 bool qce_f64g_shape(int MP, int NP);
 int qce_f64g_waves();  // waves per workgroup of k_est_all_f64g (tile = 16 x waves samples; 8 / waves workgroups per CU)
 long long qce_pack_f64g_bytes(int MP, int NP, int has_mean);

@@ -126,6 +126,30 @@ int kshard_reserve_cus() {
   return v < 0 ? 0 : v;
 }
 
+// Test hook QCE_KSHARD_EMULATE_WORLD="W[:R]" (a world-1 communicator only): lay the step's rows out as rank R of W
+// ranks would -- the shard computes its components over all B rows, but its reduce-scatter takes and returns only
+// the rank's B / W rows and only those are finalised -- so one GPU rehearses the per-rank work of a W-GPU step
+// (the collective's wire time is the part one GPU cannot show)
+bool kshard_emulated(int* world, int* rank) {
+  const char* e = getenv("QCE_KSHARD_EMULATE_WORLD");
+  if (!e || !*e) return false;
+  char* end = nullptr;
+  const long w = strtol(e, &end, 10);
+  if (end == e) return false;
+  long r = 0;
+  if (*end == ':') {
+    char* e2 = nullptr;
+    r = strtol(end + 1, &e2, 10);
+    if (e2 == end + 1 || *e2) return false;
+  } else if (*end) {
+    return false;
+  }
+  if (w < 2 || w > 4096 || r < 0 || r >= w) return false;
+  *world = (int)w;
+  *rank = (int)r;
+  return true;
+}
+
 void slice_of(int K, int world, int rank, int* lo, int* hi) {
   const int base = K / world, rem = K % world;
   *lo = rank * base + (rank < rem ? rank : rem);
@@ -334,6 +358,9 @@ struct qce_kshard {
   int used_valid[2] = {0, 0};
   qce_comm* c = nullptr;
   int K = 0, lo = 0, hi = 0, Kmax = 0;
+  int lw = 1, lr = 0;  // world / rank the rows are laid out for: the communicator's, or QCE_KSHARD_EMULATE_WORLD's
+  int reserve = 0;     // CUs the step's persistent kernels leave to the communication stream (unless the caller set
+                       // QCE_OPT_RESERVE_CUS on the model; applied per launch, the model is not modified)
   hipStream_t cs = nullptr;  // communication stream: the chunks' collectives and row finalisation
   std::vector<hipEvent_t> ev_chunk;
   hipEvent_t ev_done = nullptr;
@@ -438,6 +465,16 @@ int collective(qce_comm* c, int op, double* send, double* recv, long long count,
   return QCE_OK;
 }
 
+// the step's CU reservation for the duration of one launch call (the launches read it when they size the grid)
+struct ReserveScope {
+  qce_model* m;
+  int prev;
+  ReserveScope(qce_model* mm, int reserve) : m(mm), prev(mm->reserve_cus) {
+    if (!m->reserve_set) m->reserve_cus = reserve;
+  }
+  ~ReserveScope() { m->reserve_cus = prev; }
+};
+
 hipStream_t ks_stream(qce_kshard* ks, void* stream) {
   if (stream) return (hipStream_t)stream;
   return ks->m->stream;
@@ -486,7 +523,9 @@ int reduce_chunks(qce_kshard* ks, const std::vector<Chunk>& L, bool scatter, int
   double* send = ks->pkb[ks->pkp].p + ch.pk_off * W;
   const double* rows;
   if (scatter) {
-    const long long q = ch.npad / c->world;
+    const long long q = ch.npad / ks->lw;
+    // an emulated layout on a world-1 communicator: the rank's own q rows are the whole world-1 reduce-scatter
+    if (ks->lw != c->world) send += (long long)ks->lr * q * W;
     double* recv = ks->rs.p + ch.rs_off * W;
     KS_RC(collective(c, QCE_COLL_REDUCE_SCATTER_SUM, send, recv, q * W, ks->cs, premul));
     rows = recv;
@@ -561,11 +600,11 @@ int step_all(qce_kshard* ks, qce_model* m, const double2* y, long long B, int ch
              hipStream_t st, bool rowshift) {
   qce_comm* c = ks->c;
   const int N = m->N, M = m->M, W = 2 * N + 2;
-  std::vector<Chunk> L = chunk_layout(B, chunks, c->world, c->rank, scatter);
+  std::vector<Chunk> L = chunk_layout(B, chunks, ks->lw, ks->lr, scatter);
   long long pk_rows = 0, rs_rows = 0;
   for (const Chunk& ch : L) {
     pk_rows += ch.npad;
-    if (scatter) rs_rows += ch.npad / c->world;
+    if (scatter) rs_rows += ch.npad / ks->lw;
   }
   KBuf<double>& pkbuf = ks->pkb[ks->pkp];
   KS_HIP(pkbuf.ensure((size_t)pk_rows * W));
@@ -601,6 +640,7 @@ int step_all(qce_kshard* ks, qce_model* m, const double2* y, long long B, int ch
       bool ok = false;
       if (!ks->local_chol) {
         KS_RC(timed_begin(ks, st));
+        ReserveScope rsv(m, ks->reserve);
         ok = guarded(ks, qce_estimate_partial_shifted(m, reinterpret_cast<const double*>(y + ch.lo * M), n,
                                                       ks->step_shift.p + 2 * ks->pkp, pk, QCE_IO_DEVICE, st), &hard);
         if (hard) return hard;
@@ -621,6 +661,9 @@ int step_select(qce_kshard* ks, const double2* y, long long B, int mode, double 
   const int N = m->N, Kl = m->K, W = 2 * N;
   int kmode, nsel = 0;
   double p = 0.0;
+  if (ks->lw != c->world)
+    return qce_set_error(QCE_ENOTIMPL, "QCE_KSHARD_EMULATE_WORLD rehearses the 'all' mode only");
+  ReserveScope rsv(m, ks->reserve);
   if (mode == QCE_MODE_TOPN) {
     if (param < 1.0 || param != floor(param)) return qce_set_error(QCE_EARG, "top-n needs an integer n >= 1");
     nsel = param > 1e9 ? 1000000000 : (int)param;
@@ -811,8 +854,11 @@ int qce_kshard_create(qce_model* shard, qce_comm* comm, int K_total, qce_kshard*
     return qce_set_error(QCE_EARG, "the shard model must hold components [" + std::to_string(lo) + ", " +
                                        std::to_string(hi) + ") of the balanced split (qce_kshard_slice)");
   DevGuard g(shard->device);
-  if (comm->kind == QCE_COMM_RCCL && comm->world > 1) shard->reserve_cus = kshard_reserve_cus();
   qce_kshard* ks = new qce_kshard();
+  ks->lw = comm->world;
+  ks->lr = comm->rank;
+  if (comm->world == 1) (void)kshard_emulated(&ks->lw, &ks->lr);
+  if (comm->kind == QCE_COMM_RCCL && ks->lw > 1) ks->reserve = kshard_reserve_cus();
   ks->m = shard;
   ks->mods[0] = shard;
   ks->device = shard->device;
@@ -922,7 +968,6 @@ int qce_kshard_set_spare(qce_kshard* ks, qce_model* spare) {
     KS_HIP(hipEventCreateWithFlags(&ks->ev_used[i], hipEventDisableTiming));
   }
   ks->mods[1] = spare;
-  spare->reserve_cus = ks->mods[0]->reserve_cus;
   return QCE_OK;
 }
 

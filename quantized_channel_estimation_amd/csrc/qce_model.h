@@ -31,8 +31,10 @@ struct DevBuf {
 struct qce_model {
   int K = 0, N = 0, device = 0;
   int a_identity_n = 0;   // m->A holds I_N (skips the upload + sync of a repeated A = NULL prepare)
-  const void* q0_zero = nullptr;    // zero-mean model: the q0 / bvec buffers at these addresses hold zeros
-  const void* bvec_zero = nullptr;  // (the prepare then skips their three launches)
+  // zero-mean model: the first q0_zeroed / bvec_zeroed elements of q0 / bvec hold zeros (the prepare then skips
+  // their three launches).  Counted in elements, not remembered by address: a DevBuf::ensure that grows
+  // the buffer may get the old address back from hipMalloc, and the grown tail must be zeroed again
+  size_t q0_zeroed = 0, bvec_zeroed = 0;
   int packs_valid = 0;    // pack32 / pack64 built for the current prepare (lazy: 'all' mode never needs them)
   QcePrepareArgs pack_args{};
   int beta_first = 0;  // QCE_OPT_BETA_FIRST: multi-bit Cr mixes with the first gain (blmmse.py:53, :86)
@@ -82,6 +84,7 @@ struct qce_model {
   int wt_valid = 0;
   int cu_count = 256;
   int reserve_cus = 0;  // QCE_OPT_RESERVE_CUS: CUs the persistent grids leave to a concurrent communication stream
+  int reserve_set = 0;  // the caller set QCE_OPT_RESERVE_CUS (a K-shard step then keeps the caller's value)
   int sched_cus() const { return cu_count - reserve_cus > 8 ? cu_count - reserve_cus : 8; }
   // dimensions beyond the fused kernels' 256 (qce_big.hip): GEMM-based FP64 path
   int big = 0;

@@ -173,6 +173,17 @@ class ComponentShardEstimator:
                     spare.set_precision(precision)
                 self.native.set_spare(spare)
 
+    def close(self):
+        """Release the library's K-shard step and this rank's table sets (the communicator stays the caller's).  Call
+        it before the process ends: teardown left to exit-time destructors is what VERDICT r5 #4 traced a crash to."""
+        if self.native is not None:
+            spare = getattr(self.native, "spare", None)
+            self.native.close()
+            if spare is not None:
+                spare.close()
+        self.dev.close()
+        self._bufs = {}
+
     def _on_gpu(self):
         return getattr(self.dev, "device_type", "cuda") == "cuda"
 

@@ -230,7 +230,8 @@ def test_f64_selective_modes_vs_oracle(K, N, pilots, B, n_bits, mean):
 
 
 @pytest.mark.parametrize("N,M_pilots,mean", [(64, 1, False), (64, 1, True), (48, 1, True), (32, 1, False),
-                                             (16, 1, True), (20, 1, False), (32, 2, True), (16, 4, False)])
+                                             (16, 1, True), (20, 1, False), (32, 2, True), (16, 4, False),
+                                             (128, 1, False), (128, 1, True), (100, 1, True), (72, 1, False)])
 def test_f64_3m_matches_4m_and_oracle(N, M_pilots, mean, monkeypatch):
     """The 3M (Gauss) kernel k_est_all_f64g against the 4M kernel k_est_all_f64 (QCE_F64_3M=0 at prepare) and the FP64
     oracle: same FP64 computation up to rounding (1e-12 relative between the kernels, 1e-9 vs the oracle), for every
@@ -324,3 +325,30 @@ def test_bench_sweep_line():
     r = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert r["config"]["points"] == 7 and r["max_rel_dev_vs_serial"] < 1e-12
     assert r["parity"]["rel_fro"] < 1e-9 and r["ms_per_snr_point"] > 0
+
+
+@pytest.mark.parametrize("mean", [False, True])
+def test_f64h_whole_rounds_and_kshard_rows(mean, monkeypatch):
+    """The padded-128 3M kernel k_est_all_f64h (row halves, y in LDS) with whole-tile rounds AND a stream-K tail
+    (B = 40 000: 625 tiles of 64 over the persistent grid), and its shifted packed K-shard rows: equal to the 4M
+    wave-pair kernel (QCE_F64_3M=0) within 1e-12, to the FP64 oracle within 1e-9 on 300 rows."""
+    _gpu_or_skip()
+    from oracle import qce_oracle as O
+    from quantized_channel_estimation_amd import _lib
+    K, N, B = 8, 128, 40000
+    means, covs, w, h, y, _ = _synthetic(K, N, B, 913, 1, mean=mean)
+    dm = _lib.DeviceModel(means, covs, w)
+    dm.prepare(None, 5.0, 1.0)
+    assert dm.kernel() == "f64_3m"
+    h3 = dm.estimate(y)
+    pk3 = dm.partial_shifted(y, dm.cconst_max())
+    monkeypatch.setenv("QCE_F64_3M", "0")
+    dm.prepare(None, 5.0, 1.0)
+    assert dm.kernel() == "f64_4m"
+    h4 = dm.estimate(y)
+    pk4 = dm.partial_shifted(y, dm.cconst_max())
+    assert rel_fro(h3, h4) < 1e-12, rel_fro(h3, h4)
+    assert rel_fro(pk3, pk4) < 1e-12, rel_fro(pk3, pk4)
+    ho = O.estimate(means, covs, w, y[:300], 5.0, N, None, "all", 1)
+    assert rel_fro(h3[:300], ho) < F64_TOL
+    dm.close()

@@ -1,8 +1,16 @@
 #!/usr/bin/env python3
 """One rank's K-shard step through the library's communicator (qce_kshard_*) at the metric geometry, world 1 over
-RCCL by default: prepare (+ shift MAX all-reduce), chunked partials + reduce-scatters, flag MAX, finish.  Prints one
-JSON line (per-step time, summed partial-kernel time, parity of 512 rows against the FP64 oracle).  Used under
-rocprofv3 --kernel-trace to show the RCCL kernels next to the estimate kernels (profiles/r04_kshard_native_*)."""
+RCCL by default: prepare (+ the step's shift MAX), chunked partials + reduce-scatters, flag MAX, finish.  Prints one
+JSON line (per-step time, summed partial-kernel time, parity of 512 rows against the FP64 oracle and, with
+--emulate-world, against the single-GPU estimate of the same rows).
+
+--emulate-world W[:R] (QCE_KSHARD_EMULATE_WORLD) lays the rows out as rank R of a W-GPU step: the shard's K
+components over all B rows, but the reduce-scatter and the finalisation of only the rank's B / W rows -- the per-rank
+work of the W-GPU step without its wire time.  --K is then the per-rank component count.
+Used under rocprofv3 --kernel-trace to show the RCCL kernels next to the estimate kernels (profiles/r0*_kshard_*).
+
+The K-shard, its table sets and the communicator are closed explicitly before exit (--no-close leaves them to the
+process teardown: the exit-time test of VERDICT r5 #4)."""
 import argparse
 import json
 import os
@@ -20,15 +28,21 @@ def main():
     ap.add_argument("--K", type=int, default=128)
     ap.add_argument("--N", type=int, default=64)
     ap.add_argument("--B", type=int, default=100_000)
-    ap.add_argument("--chunks", type=int, default=2)
+    ap.add_argument("--chunks", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--kind", default="rccl", choices=["rccl", "host"])
     ap.add_argument("--single-buffer", action="store_true", help="no spare table set (prepare not overlapped)")
-    ap.add_argument("--reserve", type=int, default=0,
-                    help="CUs the shard's grid leaves free (QCE_OPT_RESERVE_CUS; the library sets 16 at world > 1)")
+    ap.add_argument("--reserve", type=int, default=-1,
+                    help="CUs the shard's grid leaves free (QCE_OPT_RESERVE_CUS; default: the library's K-shard "
+                         "default, 16 at world > 1 or an emulated world)")
+    ap.add_argument("--emulate-world", default="", help="W[:R]: rehearse rank R of a W-GPU step on this world-1 rank")
+    ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-close", action="store_true", help="exit without closing the K-shard / communicator")
     a = ap.parse_args()
+    if a.emulate_world:
+        os.environ["QCE_KSHARD_EMULATE_WORLD"] = a.emulate_world
     import torch
-    from quantized_channel_estimation_amd import inputs
+    from quantized_channel_estimation_amd import _lib, inputs
     from quantized_channel_estimation_amd.sharding import ComponentShardEstimator, make_comm
     means, covs, w = inputs.synthetic_model(a.K, a.N)
     rng = np.random.default_rng(5)
@@ -43,7 +57,7 @@ def main():
         dist.init_process_group("gloo", rank=0, world_size=1)
     comm = make_comm(0, 1, 0, kind=a.kind)
     est = ComponentShardEstimator(means, covs, w, 0, 1, device=0, comm=comm, double_buffer=not a.single_buffer)
-    if a.reserve:
+    if a.reserve >= 0:
         est.dev.reserve_cus(a.reserve)
         if getattr(est.native, "spare", None) is not None:
             est.native.spare.reserve_cus(a.reserve)
@@ -59,18 +73,31 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         est.prepare(None, 5.0, 1)
-        res = est.estimate(yd, chunks=a.chunks, scatter=True, sync=False)
+        est.estimate(yd, chunks=a.chunks, scatter=True, sync=False)
     rows, hk = est.finish()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
     kms, nl = est.native.kernel_ms()
-    from oracle import qce_oracle as O
-    r = rows.cpu().numpy()[:512]
-    ho = O.estimate(means, covs, w, y[r], 5.0, a.N, None, "all", 1)
-    err = float(np.linalg.norm(hk[:512].cpu().numpy() - ho) / np.linalg.norm(ho))
-    print(json.dumps(dict(kind=a.kind, double_buffer=not a.single_buffer, K=a.K, N=a.N, B=a.B, chunks=a.chunks, reserve_cus=a.reserve, steps=a.steps, ms_per_step=dt * 1e3,
-                          partial_kernel_ms_per_step=kms / a.steps, launches=nl, est_per_s=a.B / dt,
-                          parity_rel_fro=err)), flush=True)
+    r = rows.cpu().numpy()
+    hkn = hk.cpu().numpy()
+    rec = dict(kind=a.kind, double_buffer=not a.single_buffer, K=a.K, N=a.N, B=a.B, chunks=a.chunks,
+               reserve_cus=a.reserve, emulate_world=a.emulate_world or None, rows=int(r.size), steps=a.steps,
+               ms_per_step=dt * 1e3, partial_kernel_ms_per_step=kms / a.steps, launches=nl,
+               est_per_s_rank_rows=r.size / dt)
+    if not a.no_parity:
+        from oracle import qce_oracle as O
+        ho = O.estimate(means, covs, w, y[r[:512]], 5.0, a.N, None, "all", 1)
+        rec["parity_rel_fro"] = float(np.linalg.norm(hkn[:512] - ho) / np.linalg.norm(ho))
+        # the same rows through the single-GPU estimate of the same mixture (K-shard vs one GPU)
+        dm = _lib.DeviceModel(means, covs, w, device=0)
+        dm.prepare(None, 5.0, 1)
+        h1 = dm.estimate(yd[torch.from_numpy(r).cuda()]).cpu().numpy()
+        rec["vs_single_gpu_rel_fro"] = float(np.linalg.norm(hkn - h1) / np.linalg.norm(h1))
+        dm.close()
+    print(json.dumps(rec), flush=True)
+    if not a.no_close:
+        est.close()
+        comm.close()
 
 
 if __name__ == "__main__":
