@@ -642,8 +642,25 @@ class KShard:
         check(load().qce_kshard_create(model.handle, comm.handle, int(K_total), ctypes.byref(h)))
         self._h, self.model, self.comm, self.K = h, model, comm, int(K_total)
         self._keep = None
+        self._own = None  # private torch stream standing in for torch's null stream (_stream)
         self.layout_world, self.layout_rank = kshard_layout(comm.world, comm.rank)
         _live["kshard"].add(self)
+
+    def _stream(self, stream):
+        """(handle, torch's current stream) of the stream a K-shard call runs on: the caller's, else torch's current
+        stream.  A null handle would mean "the model's own stream" to the library -- unordered with torch's work (y
+        uploaded on the null stream could still be in flight) -- so torch's null stream is replaced by a private torch
+        stream that waits for it."""
+        import torch
+        dev = torch.device("cuda", self.model.device)
+        cur = torch.cuda.current_stream(dev)
+        s = int(stream) if stream else cur.cuda_stream
+        if s == 0:
+            if self._own is None:
+                self._own = torch.cuda.Stream(dev)
+            self._own.wait_stream(cur)
+            s = self._own.cuda_stream
+        return s, cur
 
     def set_spare(self, spare):
         """Double-buffered tables: `spare` another DeviceModel of the same shard (qce_kshard_set_spare)."""
@@ -678,6 +695,7 @@ class KShard:
             lab = np.ascontiguousarray(labels, dtype=np.float64)
             thr = np.ascontiguousarray(thresholds, dtype=np.float64)
             nlev = lab.size
+        stream, _ = self._stream(stream)
         check(load().qce_kshard_prepare(self._h, ptr(a), int(M), float(snr_db), float(n_bits), int(quant_kind),
                                         ptr(thr), ptr(lab), int(nlev), stream))
         m.M = M
@@ -685,12 +703,10 @@ class KShard:
     def estimate(self, y, mode=MODE_ALL, param=0.0, chunks=2, scatter=True, out=None, stream=None):
         """y (B, M) complex128 CUDA tensor (the same on every rank) -> (rows, h): h the estimates of the global rows
         `rows` (a list of (r0, r1) ranges in h's row order).  Asynchronous on `stream` (default: torch's current
-        stream of y's device); finish() is the sync point."""
+        stream of y's device, see _stream); finish() is the sync point."""
         import torch
         B = y.shape[0]
-        cur = torch.cuda.current_stream(y.device)
-        if stream is None:
-            stream = cur.cuda_stream
+        stream, cur = self._stream(stream)
         ch = int(chunks) if mode == MODE_ALL else 1
         rows = kshard_rows(B, ch, self.layout_world, self.layout_rank, scatter)
         n = sum(b - a for a, b in rows)

@@ -37,44 +37,33 @@
 
 namespace {
 
-// virtual blocks per half and component: 300 (+ 8 with means), padded to a multiple of E + 1 so the register ring's
-// slot of block b is b mod (E + 1) in every component (the stream runs on across components)
-constexpr __host__ __device__ int f64h_vb(int hmi) {
-  return (300 + 8 * hmi + QCE_F64H_E) / (QCE_F64H_E + 1) * (QCE_F64H_E + 1);
-}
-
 // GL tile i (0..3) of half h
 constexpr __host__ __device__ int f64h_gl_tile(int h, int i) {
   return h == 0 ? (i == 0 ? 7 : i == 1 ? 0 : i == 2 ? 5 : 2) : (i == 0 ? 6 : i == 1 ? 1 : i == 2 ? 4 : 3);
 }
 
-struct BlockInfoH {
-  int kind, T, u, j;  // kind: 0 GL data (T global tile), 1 GL mean, 2 GW data (T local tile 0..3), 3 GW bias, 4 none
-  bool fold;          // the last GL block of a tile: fold its rows into the quad form
-  bool ustart;        // the first block of a unit: its y operands are read (two blocks earlier)
-};
+// GL units per half: sum over its tiles of 2T + 2 (+ one mean unit per tile with means) -- 36 / 40 for both halves
+constexpr __host__ __device__ int f64h_glu(int hmi) { return 36 + 4 * hmi; }
 
-__host__ __device__ constexpr BlockInfoH block_info_h(int hmi, int h, int v) {
+// unit p (0 .. f64h_glu - 1) of half h's GL stream
+struct UnitH {
+  int T, u;   // GL tile, unit of the tile (two k-steps 2u, 2u + 1)
+  bool mean;  // the tile's mean unit (the -q0 column, against the constant y row of the LDS tile)
+  bool last;  // the tile's last unit: fold its rows into the quad form after it
+};
+__host__ __device__ constexpr UnitH f64h_unit(int hmi, int h, int p) {
   for (int i = 0; i < 4; ++i) {
-    const int T = f64h_gl_tile(h, i), L = 3 * (2 * T + 2);
-    if (v < L) return BlockInfoH{0, T, v / 3, v % 3, hmi == 0 && v == L - 1, v % 3 == 0};
-    v -= L;
-    if (hmi) {
-      if (v == 0) return BlockInfoH{1, T, 0, 0, true, false};
-      v -= 1;
-    }
+    const int T = f64h_gl_tile(h, i), n = 2 * T + 2 + hmi;
+    if (p < n) return UnitH{T, p, hmi && p == n - 1, p == n - 1};
+    p -= n;
   }
-  if (v < 192) return BlockInfoH{2, (v % 12) % 4, v / 12, (v % 12) / 4, false, v % 12 == 0};
-  v -= 192;
-  if (hmi && v < 4) return BlockInfoH{3, v, 0, 0, false, false};
-  return BlockInfoH{4, 0, 0, 0, false, false};
+  return UnitH{0, 0, false, false};
 }
 
-// unit starts in blocks [0, v) of half h's stream (the y-operand slot of a unit is this count mod 2)
-__host__ __device__ constexpr int f64h_useq(int hmi, int h, int v) {
-  int n = 0;
-  for (int b = 0; b < v; ++b) n += block_info_h(hmi, h, b).ustart ? 1 : 0;
-  return n;
+// virtual blocks per half and component: 3 per GL unit, 192 GW (+ 4 bias with means), padded to a multiple of E + 1
+// so the register ring's slot of block b is b mod (E + 1) in every component (the stream runs on across components)
+constexpr __host__ __device__ int f64h_vb(int hmi) {
+  return (3 * f64h_glu(hmi) + 192 + 4 * hmi + QCE_F64H_E) / (QCE_F64H_E + 1) * (QCE_F64H_E + 1);
 }
 
 QCE_DEV __amdgpu_buffer_rsrc_t f64h_rsrc(const void* p, unsigned bytes) {
@@ -98,7 +87,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   constexpr int HMI = HM ? 1 : 0;
   constexpr int TS = 64;                       // samples per tile: 4 groups of 16
   constexpr int KS = 32;                       // k-steps at padded M = 128
-  constexpr int GLV = 108 + 4 * HMI;           // GL blocks per half
+  constexpr int GLU = f64h_glu(HMI);           // GL units per half
+  constexpr int GLV = 3 * GLU;                 // GL blocks per half
   constexpr int GWV = 192 + 4 * HMI;           // GW blocks per half
   constexpr int VB = f64h_vb(HMI);             // virtual blocks per half and component
   constexpr unsigned STRIDE = (unsigned)VB * 2048u;
@@ -106,9 +96,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   constexpr int D = 2;                         // y operands read D blocks ahead of their unit
   constexpr double RESCALE = 32.0;             // lazy max: rescale only when lp exceeds m by this
   static_assert(E >= 1 && E < GLV && D < 3, "prefetch distances");
-  static_assert(f64h_useq(HMI, 0, GLV) == 36 && f64h_useq(HMI, 1, GLV) == 36, "unit count of the GL halves");
-  static_assert((36 + 16) % 2 == 0, "y-operand slots repeat per component");
-  __shared__ __attribute__((aligned(16))) double2 ylds[4][KS][64];  // the tile's y as (hs, hd), [group][k-step][lane]
+  static_assert((GLU + 16) % 2 == 0, "y-operand slots repeat per component");
+  // the tile's y as (hs, hd), [group][k-step][lane]; rows KS, KS + 1: the mean unit's constant operands (hs = hd = 1
+  // in lane group 0: R' += Lm, I' += Lp, K1 += Ls (hs - hd) = 0)
+  __shared__ __attribute__((aligned(16))) double2 ylds[4][KS + 2][64];
   __shared__ double qx[2][8][64];  // the halves' quad-form partials, alternating by component parity
   __shared__ double etab[32];      // 2^(j/32) for exp_tab64
 
@@ -117,6 +108,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int hh = wave & 1, sg = wave >> 1;  // row half, sample group (wave-uniform)
   const int g = lane >> 4, col = lane & 15;
   if (threadIdx.x < 32) etab[threadIdx.x] = exp2((double)threadIdx.x / 32.0);  // visible after the first barrier
+  if (hh == 0) {
+    ylds[sg][KS][lane] = g == 0 ? make_double2(1.0, 1.0) : make_double2(0.0, 0.0);
+    ylds[sg][KS + 1][lane] = make_double2(0.0, 0.0);
+  }
   const long long P = gridDim.x, w = blockIdx.x;
   const long long tiles = (B + TS - 1) / TS;
   const long long tail0 = (long long)R * P;
@@ -176,12 +171,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int T = 0; T < 4; ++T) ok[T] = orr[T] = oi[T] = f64x4{0.0, 0.0, 0.0, 0.0};
     double m = QCE_NEG_INF, ssum = 0.0;
 
-    // first E table blocks and the first unit's y operands of the segment's first component
+    // first E table blocks and the first unit's y operands (k-steps 0, 1 in both halves) of the first component
     __amdgpu_buffer_rsrc_t rs = rsrc_of(klo);
     double2 buf[E + 1];
 #pragma unroll
     for (int i = 0; i < E; ++i) buf[i] = f64h_ld(rs, voff, (unsigned)i * 2048u);
-    double2 yv[2][2];  // [slot][k-step of the unit]: (hs, hd)
+    double2 yv[2][2];  // [unit parity][k-step of the unit]: (hs, hd)
     yv[0][0] = yl[0];
     yv[0][1] = yl[64];
     yv[1][0] = yv[1][1] = make_double2(0.0, 0.0);
@@ -196,6 +191,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       f64x4 k1 = f64x4{0.0, 0.0, 0.0, 0.0}, rr = k1, ii = k1;
       double qp = 0.0, p = 0.0;
       double pr0 = 0.0, ps0 = 0.0, pd0 = 0.0, pr1 = 0.0, ps1 = 0.0, pd1 = 0.0;
+      // One instruction stream for both halves: every GL unit is three blocks with the same accumulator pattern, so
+      // the halves differ only in data -- the table blocks, the k-steps their y operands are read from (a wave-uniform
+      // select of two constants) and where a tile's rows are folded (a wave-uniform select of the fold's result).
       static_for(
           [&](auto vc) {
             constexpr int v = decltype(vc)::value;
@@ -207,88 +205,92 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
               buf[(v + E) % (E + 1)] = f64h_ld(rn, voff, (unsigned)(v + E - VB) * 2048u);
             }
             const double2 a = buf[v % (E + 1)];
-            // y operands of the unit starting D blocks ahead (the next component's first unit: k-steps 0, 1)
-            auto yread = [&](auto hc) {
-              constexpr int H = decltype(hc)::value;
-              if constexpr (v + D < VB) {
-                constexpr BlockInfoH nb = block_info_h(HMI, H, v + D);
-                if constexpr (nb.ustart) {
-                  constexpr int sl = f64h_useq(HMI, H, v + D) & 1;
-                  yv[sl][0] = yl[(2 * nb.u) * 64];
-                  yv[sl][1] = yl[(2 * nb.u + 1) * 64];
-                }
-              } else if constexpr (v + D == VB) {
-                yv[0][0] = yl[0];
-                yv[0][1] = yl[64];
-              }
-            };
-            if constexpr (v < GLV) {
-              // GL: the half's own tiles (wave-uniform branch: the two streams differ in their k-steps and folds)
-              auto gl = [&](auto hc) {
-                constexpr int H = decltype(hc)::value;
-                constexpr BlockInfoH bi = block_info_h(HMI, H, v);
-                if constexpr (bi.kind == 0) {
-                  constexpr int sl = (f64h_useq(HMI, H, v) - (bi.ustart ? 0 : 1)) & 1;
-                  const double2 y0 = yv[sl][0], y1 = yv[sl][1];
-                  if constexpr (bi.j == 0) {
-                    k1 = mfma16x16x4d(a.x, fma(y0.y, neg1, y0.x), k1);
-                    rr = mfma16x16x4d(a.y, y0.x, rr);
-                  } else if constexpr (bi.j == 1) {
-                    ii = mfma16x16x4d(a.x, y0.y, ii);
-                    k1 = mfma16x16x4d(a.y, fma(y1.y, neg1, y1.x), k1);
-                  } else {
-                    rr = mfma16x16x4d(a.x, y1.x, rr);
-                    ii = mfma16x16x4d(a.y, y1.y, ii);
-                  }
-                } else if constexpr (bi.kind == 1) {  // mean column (-q0): B = 1 in lane group 0
-                  const double one = g == 0 ? 1.0 : 0.0;
-                  rr = mfma16x16x4d(a.x, one, rr);
-                  ii = mfma16x16x4d(a.y, one, ii);
-                }
-                yread(hc);
-                if constexpr (bi.fold) {
+            if constexpr (v < GLV) {  // GL unit U, block j
+              constexpr int U = v / 3, j = v % 3;
+              const double2 y0 = yv[U & 1][0], y1 = yv[U & 1][1];
+              if constexpr (j == 0) {
+                k1 = mfma16x16x4d(a.x, fma(y0.y, neg1, y0.x), k1);
+                rr = mfma16x16x4d(a.y, y0.x, rr);
+              } else if constexpr (j == 1) {
+                ii = mfma16x16x4d(a.x, y0.y, ii);
+                k1 = mfma16x16x4d(a.y, fma(y1.y, neg1, y1.x), k1);
+              } else {
+                rr = mfma16x16x4d(a.x, y1.x, rr);
+                ii = mfma16x16x4d(a.y, y1.y, ii);
+                constexpr bool f0 = f64h_unit(HMI, 0, U).last, f1 = f64h_unit(HMI, 1, U).last;
+                if constexpr (f0 || f1) {  // the end of a tile of one or both halves: |z|^2 of its rows
+                  double qn = qp;
 #pragma unroll
                   for (int i = 0; i < 4; ++i) {
                     const double zr = k1[i] + rr[i], zi = k1[i] + ii[i];
-                    qp = fma(zr, zr, qp);
-                    qp = fma(zi, zi, qp);
+                    qn = fma(zr, zr, qn);
+                    qn = fma(zi, zi, qn);
+                  }
+                  if constexpr (f0 && f1) {
+                    qp = qn;
+                    k1 = rr = ii = f64x4{0.0, 0.0, 0.0, 0.0};
+                  } else {
+                    const bool fold = hh == 0 ? f0 : f1;  // wave-uniform
+                    qp = fold ? qn : qp;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                      k1[i] = fold ? 0.0 : k1[i];
+                      rr[i] = fold ? 0.0 : rr[i];
+                      ii[i] = fold ? 0.0 : ii[i];
+                    }
                   }
                   asm volatile("" : "+v"(qp));
-                  k1 = rr = ii = f64x4{0.0, 0.0, 0.0, 0.0};
                 }
-              };
-              if (hh == 0) gl(ICH<0>{});
-              else gl(ICH<1>{});
+              }
             } else {
-              constexpr BlockInfoH bi = block_info_h(HMI, 0, v);
-              constexpr int T = bi.T;
-              if constexpr (bi.kind == 2) {  // GW data: B operands formed once per unit
-                constexpr int sl = (f64h_useq(HMI, 0, v) - (bi.ustart ? 0 : 1)) & 1;
-                if constexpr (T == 0 && bi.j == 0) {
+              constexpr int r = v - GLV;
+              if constexpr (r < 192) {  // GW data, unit u, block j, local tile T: B operands formed once per unit
+                constexpr int u = r / 12, j = (r % 12) / 4, T = (r % 12) % 4, sl = u & 1;
+                if constexpr (T == 0 && j == 0) {
                   ps0 = p * yv[sl][0].x;
                   pd0 = p * yv[sl][0].y;
                   pr0 = ps0 - pd0;
-                } else if constexpr (T == 0 && bi.j == 1) {
+                } else if constexpr (T == 0 && j == 1) {
                   ps1 = p * yv[sl][1].x;
                   pd1 = p * yv[sl][1].y;
                   pr1 = ps1 - pd1;
                 }
-                if constexpr (bi.j == 0) {
+                if constexpr (j == 0) {
                   ok[T] = mfma16x16x4d(a.x, pr0, ok[T]);
                   orr[T] = mfma16x16x4d(a.y, ps0, orr[T]);
-                } else if constexpr (bi.j == 1) {
+                } else if constexpr (j == 1) {
                   oi[T] = mfma16x16x4d(a.x, pd0, oi[T]);
                   ok[T] = mfma16x16x4d(a.y, pr1, ok[T]);
                 } else {
                   orr[T] = mfma16x16x4d(a.x, ps1, orr[T]);
                   oi[T] = mfma16x16x4d(a.y, pd1, oi[T]);
                 }
-              } else if constexpr (bi.kind == 3) {  // GW bias column (b): B = p in lane group 0
+              } else if constexpr (HM && r < 196) {  // GW bias column (b): B = p in lane group 0
+                constexpr int T = r - 192;
                 const double pone = g == 0 ? p : 0.0;
                 orr[T] = mfma16x16x4d(a.x, pone, orr[T]);
                 oi[T] = mfma16x16x4d(a.y, pone, oi[T]);
               }
-              yread(ICH<0>{});  // GW blocks are the same for both halves
+            }
+            // y operands of the unit starting D blocks ahead, into its parity slot (the slot in use is the other one)
+            constexpr int vn = v + D;
+            if constexpr (vn < GLV && vn % 3 == 0) {
+              constexpr int Un = vn / 3;
+              constexpr UnitH n0 = f64h_unit(HMI, 0, Un), n1 = f64h_unit(HMI, 1, Un);
+              constexpr int s0 = n0.mean ? KS : 2 * n0.u, s1 = n1.mean ? KS : 2 * n1.u;
+              int su = hh == 0 ? s0 : s1;
+              asm volatile("" : "+s"(su));  // laundered: no read is CSE'd across units (register pressure)
+              yv[Un & 1][0] = yl[su * 64];
+              yv[Un & 1][1] = yl[su * 64 + 64];
+            } else if constexpr (vn >= GLV && vn < GLV + 192 && (vn - GLV) % 12 == 0) {
+              constexpr int un = (vn - GLV) / 12;
+              int su = 2 * un;
+              asm volatile("" : "+s"(su));
+              yv[un & 1][0] = yl[su * 64];
+              yv[un & 1][1] = yl[su * 64 + 64];
+            } else if constexpr (vn == VB) {  // the next component's first unit
+              yv[0][0] = yl[0];
+              yv[0][1] = yl[64];
             }
             // after the last GL block: the halves' quad forms meet, then the online softmax (FP64), identical in
             // both waves of the group
@@ -380,33 +382,46 @@ __global__ __launch_bounds__(64) void k_pack_f64h(int M, int N, int has_mean, co
                                                   const double2* __restrict__ bvec, double* __restrict__ pack) {
   const int pb = blockIdx.x, k = blockIdx.y, lane = threadIdx.x;
   const int v = pb >> 1, hf = pb & 1, hmi = has_mean ? 1 : 0;
-  const int VB = f64h_vb(hmi);
-  const BlockInfoH bi = block_info_h(hmi, hf, v);
+  const int VB = f64h_vb(hmi), GLV = 3 * f64h_glu(hmi);
   const int r = lane & 15, gk = lane >> 4;
-  const bool isL = bi.kind <= 1;
-  const int i = 16 * (isL ? bi.T : 4 * hf + bi.T) + r;  // matrix row of the lane
-  const int rows = isL ? M : N;
   double val[2] = {0.0, 0.0};
-  if (bi.kind == 0 || bi.kind == 2) {
-    const int s0 = 2 * bi.u, s1 = s0 + 1;
-    const int wh[3][2] = {{0, 1}, {2, 0}, {1, 2}};  // 0 Ls, 1 Lm, 2 Lp
-    const int ks[3][2] = {{s0, s0}, {s0, s1}, {s1, s1}};
-    for (int e = 0; e < 2; ++e) {
-      const int j = 4 * ks[bi.j][e] + gk;
-      if (i < rows && j < M) {
-        const double2 z = isL ? Linv[((long long)k * M + i) * M + j] : W[((long long)k * N + i) * M + j];
-        const int which = wh[bi.j][e];
-        val[e] = which == 0 ? z.x + z.y : (which == 1 ? -2.0 * z.y : 2.0 * z.x);
+  // block j of a unit: the A operands of its two MFMAs, which = 0 Ls, 1 Lm, 2 Lp of k-step 2u (+ 1)
+  const int wh[3][2] = {{0, 1}, {2, 0}, {1, 2}};
+  auto entry = [&](const double2 z, int which) {
+    return which == 0 ? z.x + z.y : (which == 1 ? -2.0 * z.y : 2.0 * z.x);
+  };
+  if (v < GLV) {
+    const int U = v / 3, j = v % 3;
+    const UnitH un = f64h_unit(hmi, hf, U);
+    const int i = 16 * un.T + r;
+    if (un.mean) {  // against y = (hs, hd) = (1, 1) in lane group 0: R' += -Re q0 (j 0), I' += -Im q0 (j 1)
+      if (gk == 0 && i < M) {
+        const double2 z = q0[(long long)k * M + i];
+        if (j == 0) val[1] = -z.x;
+        if (j == 1) val[0] = -z.y;
+      }
+    } else {
+      const int s0 = 2 * un.u, ks[3][2] = {{s0, s0}, {s0, s0 + 1}, {s0 + 1, s0 + 1}};
+      for (int e = 0; e < 2; ++e) {
+        const int jj = 4 * ks[j][e] + gk;
+        if (i < M && jj < M) val[e] = entry(Linv[((long long)k * M + i) * M + jj], wh[j][e]);
       }
     }
-  } else if (bi.kind == 1 && gk == 0 && i < M) {
-    const double2 z = q0[(long long)k * M + i];
-    val[0] = -z.x;
-    val[1] = -z.y;
-  } else if (bi.kind == 3 && gk == 0 && i < N) {
-    const double2 z = bvec[(long long)k * N + i];
-    val[0] = z.x;
-    val[1] = z.y;
+  } else if (v < GLV + 192) {
+    const int rr = v - GLV, u = rr / 12, j = (rr % 12) / 4, T = (rr % 12) % 4;
+    const int i = 16 * (4 * hf + T) + r;
+    const int s0 = 2 * u, ks[3][2] = {{s0, s0}, {s0, s0 + 1}, {s0 + 1, s0 + 1}};
+    for (int e = 0; e < 2; ++e) {
+      const int jj = 4 * ks[j][e] + gk;
+      if (i < N && jj < M) val[e] = entry(W[((long long)k * N + i) * M + jj], wh[j][e]);
+    }
+  } else if (hmi && v < GLV + 196) {
+    const int i = 16 * (4 * hf + (v - GLV - 192)) + r;
+    if (gk == 0 && i < N) {
+      const double2 z = bvec[(long long)k * N + i];
+      val[0] = z.x;
+      val[1] = z.y;
+    }
   }
   *reinterpret_cast<double2*>(pack + (((long long)k * VB * 2 + pb) * 64 + lane) * 2) = make_double2(val[0], val[1]);
 }

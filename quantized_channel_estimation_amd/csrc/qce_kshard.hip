@@ -9,7 +9,8 @@
 // shift M_r = max_{k in shard} c_k (>= every local lp_bk because the quad form is >= 0), with no collective between
 // the prepare and the kernel; the step's first collective (an 8-byte MAX on the communication stream) agrees on
 // M* = max_r M_r, and every SUM multiplies the shard's rows by e^{M_r - M*} on the way in (RCCL's PreMulSum with the
-// scalar in device memory; a scaling kernel before a host transport), so one SUM of the packed rows
+// scalar in device memory for all-reduces; a scaling kernel before a reduce-scatter -- RCCL 2.26.6's PreMulSum
+// reduce-scatter drops tail elements, see reduce_chunks -- and before a host transport), so one SUM of the packed rows
 // [s e^{m - M*}, 0, acc e^{m - M*}] over the shards gives h = acc / s.  Every collective of the library is issued on
 // one communicator from one stream, so every rank issues them in the same order.  The batch is cut into chunks; chunk i's
 // reduce-scatter runs on the communication stream while chunk i+1's partial kernel runs on the compute stream.
@@ -205,6 +206,12 @@ __global__ __launch_bounds__(256) void k_ks_pack_rowshift(long long B, int N, co
   }
 }
 
+// sh = [M_r, M_r]: the shard's shift of the step's table set, the second slot the MAX's input (on the communication
+// stream, so the compute stream carries no copy between two partial kernels)
+__global__ void k_ks_shift_in(const double* __restrict__ src, double* __restrict__ sh) {
+  if (threadIdx.x < 2) sh[threadIdx.x] = *src;
+}
+
 // test hook of the exact recombination (QCE_KSHARD_SHIFT_BIAS): raise the agreed shift so rows leave the range
 __global__ void k_ks_add(double* __restrict__ v, double d) {
   if (threadIdx.x == 0) v[0] += d;
@@ -373,6 +380,8 @@ struct qce_kshard {
   hipEvent_t ev_pk[2] = {nullptr, nullptr};  // recorded on cs after the last reader of pkb[p] / step_shift[p]
   int pk_valid[2] = {0, 0};
   hipEvent_t ev_st2cs = nullptr, ev_cs2st = nullptr;
+  hipEvent_t ev_shift_read = nullptr;  // recorded on cs once a step has read its table set's shift slot (agree_shift)
+  int shift_read_valid = 0;
   KBuf<unsigned> cnt;
   double* host_fl = nullptr;  // pinned: [fl0, fl1, earlier0, earlier1] of the last step
   double last_flags[4] = {0, 0, 0, 0};  // host_fl as the last qce_kshard_finish read it
@@ -524,6 +533,16 @@ int reduce_chunks(qce_kshard* ks, const std::vector<Chunk>& L, bool scatter, int
   const double* rows;
   if (scatter) {
     const long long q = ch.npad / ks->lw;
+    // The librccl this links against (2.26.6, the one torch ships) loses the tail of a large reduce-scatter with a
+    // PreMulSum op: up to 16 doubles past a boundary that depends on the count (measured on the box,
+    // tools/rs_tail_probe.py, profiles/r06_rs_tail_probe*.jsonl; SUM, and all-reduce with PreMulSum, are exact).  Over
+    // RCCL the chunk's rows -- every row this rank contributes -- are therefore scaled by a kernel first and the
+    // reduce-scatter is a plain SUM.
+    if (premul && c->kind == QCE_COMM_RCCL) {
+      hipLaunchKernelGGL(k_ks_scale_rows, dim3(grid_for(ch.npad * W)), dim3(256), 0, ks->cs, ch.npad * W, send, premul);
+      KS_HIP(hipGetLastError());
+      premul = nullptr;
+    }
     // an emulated layout on a world-1 communicator: the rank's own q rows are the whole world-1 reduce-scatter
     if (ks->lw != c->world) send += (long long)ks->lr * q * W;
     double* recv = ks->rs.p + ch.rs_off * W;
@@ -580,12 +599,17 @@ int cs_to_st(qce_kshard* ks, hipStream_t st) {
   return QCE_OK;
 }
 
-// the step's agreed shift on the communication stream: M* = MAX over the shards of M_r (step_shift[2p] -> [2p + 1],
-// after the compute stream's copy of M_r), then the PreMulSum scalar e^{M_r - M*}
+// the step's agreed shift on the communication stream: the shard's M_r of the step's table set (behind the compute
+// stream's wait for that set's prepare) into step_shift[2p], [2p + 1]; M* = MAX over the shards in [2p + 1]; then the
+// SUMs' scalar e^{M_r - M*}.  The table set's slot is not rewritten before this has read it: the next prepare into
+// the set waits for the step's close on this stream (ev_used).
 int agree_shift(qce_kshard* ks, hipStream_t st) {
   double* sh = ks->step_shift.p + 2 * ks->pkp;
   KS_RC(st_to_cs(ks, st));
-  KS_HIP(hipMemcpyAsync(sh + 1, sh, sizeof(double), hipMemcpyDeviceToDevice, ks->cs));
+  hipLaunchKernelGGL(k_ks_shift_in, dim3(1), dim3(64), 0, ks->cs, ks->shift.p + ks->cur, sh);
+  KS_HIP(hipGetLastError());
+  KS_HIP(hipEventRecord(ks->ev_shift_read, ks->cs));
+  ks->shift_read_valid = 1;
   KS_RC(collective(ks->c, QCE_COLL_ALLREDUCE_MAX, sh + 1, sh + 1, 1, ks->cs));
   double bias = 0.0;
   if (const char* b = getenv("QCE_KSHARD_GLOBAL_BIAS")) bias = atof(b);  // tests only
@@ -641,8 +665,9 @@ int step_all(qce_kshard* ks, qce_model* m, const double2* y, long long B, int ch
       if (!ks->local_chol) {
         KS_RC(timed_begin(ks, st));
         ReserveScope rsv(m, ks->reserve);
+        // the shard's own shift M_r, read straight from the table set's slot (final once st waited for its prepare)
         ok = guarded(ks, qce_estimate_partial_shifted(m, reinterpret_cast<const double*>(y + ch.lo * M), n,
-                                                      ks->step_shift.p + 2 * ks->pkp, pk, QCE_IO_DEVICE, st), &hard);
+                                                      ks->shift.p + ks->cur, pk, QCE_IO_DEVICE, st), &hard);
         if (hard) return hard;
         KS_RC(timed_end(ks, st));
       }
@@ -875,6 +900,7 @@ int qce_kshard_create(qce_model* shard, qce_comm* comm, int K_total, qce_kshard*
   for (int i = 0; i < 2 && e == hipSuccess; ++i) e = hipEventCreateWithFlags(&ks->ev_pk[i], hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ks->ev_st2cs, hipEventDisableTiming);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&ks->ev_cs2st, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&ks->ev_shift_read, hipEventDisableTiming);
   if (e == hipSuccess) e = ks->fl.ensure(2);
   if (e == hipSuccess) e = ks->earlier.ensure(2);
   if (e == hipSuccess) e = ks->cnt.ensure(1);
@@ -906,6 +932,7 @@ int qce_kshard_destroy(qce_kshard* ks) {
   if (ks->ev_done) (void)hipEventDestroy(ks->ev_done);
   if (ks->ev_st2cs) (void)hipEventDestroy(ks->ev_st2cs);
   if (ks->ev_cs2st) (void)hipEventDestroy(ks->ev_cs2st);
+  if (ks->ev_shift_read) (void)hipEventDestroy(ks->ev_shift_read);
   for (int i = 0; i < 2; ++i) {
     if (ks->ev_pk[i]) (void)hipEventDestroy(ks->ev_pk[i]);
     if (ks->ev_prep[i]) (void)hipEventDestroy(ks->ev_prep[i]);
@@ -933,6 +960,9 @@ int qce_kshard_prepare(qce_kshard* ks, const double* A, int M, double snr_db, do
   qce_model* m = ks->mods[j];
   hipStream_t ps = dbl ? ks->ps : st;
   if (dbl && ks->used_valid[j]) KS_HIP(hipStreamWaitEvent(ps, ks->ev_used[j], 0));
+  // one table set: its shift slot is read on the communication stream at the start of each step (agree_shift), which
+  // may lag behind the compute stream; the prepare that rewrites it waits for that read
+  if (!dbl && ks->shift_read_valid) KS_HIP(hipStreamWaitEvent(ps, ks->ev_shift_read, 0));
   if (ks->pending.valid && ks->pending.model == m) ks->pending.stale = 1;  // its tables are being replaced
   ks->cur = j;
   ks->m = m;
@@ -994,8 +1024,6 @@ int qce_kshard_estimate(qce_kshard* ks, const double* y, int64_t B, int mode, do
   // parity's slot (the next prepare may overwrite the table set's slot before the comm stream gets there)
   ks->pkp ^= 1;
   if (ks->pk_valid[ks->pkp]) KS_HIP(hipStreamWaitEvent(st, ks->ev_pk[ks->pkp], 0));
-  KS_HIP(hipMemcpyAsync(ks->step_shift.p + 2 * ks->pkp, ks->shift.p + ks->cur, sizeof(double),
-                        hipMemcpyDeviceToDevice, st));
   if (const char* d = getenv("QCE_KSHARD_CS_DELAY_US")) {  // tests only
     int rate_khz = 0;
     KS_HIP(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, ks->device));
@@ -1010,12 +1038,12 @@ int qce_kshard_estimate(qce_kshard* ks, const double* y, int64_t B, int mode, do
       KS_RC(step_select(ks, yd, B, mode, mode_param, scatter != 0, hd, st));
     }
   }
-  if (dbl) {  // the table set's last reader: the next prepare into it waits for this
-    KS_HIP(hipEventRecord(ks->ev_used[ks->cur], st));
-    ks->used_valid[ks->cur] = 1;
-  }
   KS_RC(st_to_cs(ks, st));  // the flag word closes the step behind its last kernel
   KS_RC(close_step(ks));
+  if (dbl) {  // the table set's last readers (the step's kernels and its shift on cs): the next prepare into it waits
+    KS_HIP(hipEventRecord(ks->ev_used[ks->cur], ks->cs));
+    ks->used_valid[ks->cur] = 1;
+  }
   ks->pending.valid = 1;
   ks->pending.y = yd;
   ks->pending.B = B;

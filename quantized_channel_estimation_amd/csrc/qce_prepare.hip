@@ -198,14 +198,77 @@ hipError_t qce_zgemm_batched(int opa, int opb, int m, int n, int k, double2 alph
   return zgemm(opa, opb, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batch, st);
 }
 
-// Cy = C + s2 I  (A = I fast path; numerically identical to I C I^H + s2 I)
-__global__ void k_cy_identity(int N, long long total, const double2* __restrict__ C, double2* __restrict__ Cy, double s2) {
-  long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= total) return;
-  int rc = (int)(idx % ((long long)N * N));
-  double2 v = C[idx];
-  if (rc / N == rc % N) v.x += s2;
-  Cy[idx] = v;
+// The LMMSE filter for A = I (M = N <= 64) in one kernel:  V = C diag(g) Linv^H,  W = V Linv  -- the k_scale_cols +
+// two batched GEMMs of the general path, without their launches and global round trips (the prepare's post-Cholesky
+// chain is latency-bound).  Workgroup (n-block of 16 output rows, component), 4 waves = the 4 column tiles of 16: V's
+// tile of the wave (FP64 MFMA, four real products per complex k-step, operands straight from L2), V's 16 rows through
+// LDS, W's tile.  Each entry is the same FP64 dot product as the GEMM path (k-steps of 4 in order).
+__global__ __launch_bounds__(256) void k_filter_id(int M, const double2* __restrict__ C, const double2* __restrict__ Linv,
+                                                   const double* __restrict__ g, double2* __restrict__ V,
+                                                   double2* __restrict__ W) {
+  __shared__ double2 vs[16][65];
+  const int nb = blockIdx.x, k = blockIdx.y;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int q = lane >> 4, c16 = lane & 15;
+  const double2* Ck = C + (long long)k * M * M;
+  const double2* Lk = Linv + (long long)k * M * M;
+  const double* gk = g + (long long)k * M;
+  const int n = 16 * nb + c16;   // A operand row of this lane
+  const int col = 16 * wv + c16;  // B operand / output column of this lane
+  const int KS = (M + 3) / 4;     // k-steps
+  // every operand of both products issued up front (the kernel is latency-bound: a load per k-step would wait out the
+  // L2 round trip 32 times)
+  double2 av[16], bv[16], lv[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int j = 4 * s + q;
+    av[s] = bv[s] = lv[s] = make_double2(0.0, 0.0);
+    if (s < KS && j < M) {
+      if (n < M) av[s] = Ck[(long long)n * M + j];
+      if (col < M) {
+        const double2 l = Lk[(long long)col * M + j];
+        const double gj = gk[j];
+        bv[s] = make_double2(l.x * gj, -l.y * gj);
+        lv[s] = Lk[(long long)j * M + col];
+      }
+    }
+  }
+  // V[n][col] = sum_j C[n][j] conj(Linv[col][j]) g_j
+  f64x4 vr = {0.0, 0.0, 0.0, 0.0}, vi = vr;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    if (s < KS) {
+      vr = mfma16x16x4d(av[s].x, bv[s].x, vr);
+      vr = mfma16x16x4d(-av[s].y, bv[s].y, vr);
+      vi = mfma16x16x4d(av[s].x, bv[s].y, vi);
+      vi = mfma16x16x4d(av[s].y, bv[s].x, vi);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {  // D layout: row = lane / 16 + 4 r, col = lane % 16
+    const int rr = q + 4 * r;
+    vs[rr][col] = make_double2(vr[r], vi[r]);
+    if (16 * nb + rr < M && col < M) V[(long long)k * M * M + (long long)(16 * nb + rr) * M + col] = make_double2(vr[r], vi[r]);
+  }
+  __syncthreads();
+  // W[n][col] = sum_m V[n][m] Linv[m][col]
+  f64x4 wr = {0.0, 0.0, 0.0, 0.0}, wi = wr;
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    if (s < KS) {
+      const int m = 4 * s + q;
+      const double2 a = m < M ? vs[c16][m] : make_double2(0.0, 0.0);
+      wr = mfma16x16x4d(a.x, lv[s].x, wr);
+      wr = mfma16x16x4d(-a.y, lv[s].y, wr);
+      wi = mfma16x16x4d(a.x, lv[s].y, wi);
+      wi = mfma16x16x4d(a.y, lv[s].x, wi);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int rr = 16 * nb + q + 4 * r;
+    if (rr < M && col < M) W[(long long)k * M * M + (long long)rr * M + col] = make_double2(wr[r], wi[r]);
+  }
 }
 
 // X_k = Linv_k diag(g_k) (M x M): the Linv Aeff product when A = I
@@ -230,16 +293,22 @@ __global__ void k_diag_add(int M, int K, double2* __restrict__ Cy, double s2) {
 // ---------------------------------------------------------------------------
 // Bussgang gain, observation mean and Cr per component (one workgroup per k)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_gain_cr(int M, int N, const double2* __restrict__ Cy, double2* __restrict__ Cr,
+// IDA (A = I, M = N): Cy = C_k + s2 I is formed here (and stored for the tables) instead of by a kernel of its own,
+// mu_y = g mu and Aeff = diag(g) without the A products -- the same values as the general form.
+template <bool IDA>
+__global__ __launch_bounds__(256) void k_gain_cr(int M, int N, double2* __restrict__ Cy, double2* __restrict__ Cr,
                                                  double* __restrict__ gain, const double2* __restrict__ A,
                                                  const double2* __restrict__ means, double2* __restrict__ means_y,
                                                  double2* __restrict__ Aeff, int kind, int n_bits, int quant_kind,
                                                  double delta, const double* __restrict__ thr,
-                                                 const double* __restrict__ lab, int beta_first) {
+                                                 const double* __restrict__ lab, int beta_first,
+                                                 const double2* __restrict__ covs, double s2) {
   // grid (K, S): slice s of component k handles the rows i = s (mod S) of Cr, mu_y and Aeff; every slice derives
   // all M gains itself (the beta-mix needs their mean), slice 0 stores them
   const int k = blockIdx.x, tid = threadIdx.x, sl = blockIdx.y, S = gridDim.y;
-  const double2* cy = Cy + (long long)k * M * M;
+  double2* cyw = Cy + (long long)k * M * M;
+  const double2* cy = IDA ? covs + (long long)k * M * M : cyw;
+  const double s2d = IDA ? s2 : 0.0;  // added on the diagonal when Cy is formed here
   double2* cr = Cr + (long long)k * M * M;
   double* gout = gain + (long long)k * M;
   extern __shared__ double gain_lds[];  // 2 M doubles: the gains and diag(Cy)^-1/2 (any M)
@@ -248,7 +317,7 @@ __global__ __launch_bounds__(256) void k_gain_cr(int M, int N, const double2* __
   __shared__ double s_beta;
   const double PI = 3.14159265358979323846;
   for (int i = tid; i < M; i += 256) {
-    double d = cy[(long long)i * M + i].x;
+    double d = cy[(long long)i * M + i].x + s2d;
     double gi;
     if (kind == 0) {  // 1 bit (:277)
       gi = sqrt(2.0 / PI) * (1.0 / sqrt(d));
@@ -291,6 +360,10 @@ __global__ __launch_bounds__(256) void k_gain_cr(int M, int N, const double2* __
     for (int j = tid & 63; j < M; j += 64) {
     const long long e = (long long)i * M + j;
     double2 v = cy[e];
+    if (IDA) {
+      if (i == j) v.x += s2;
+      cyw[e] = v;
+    }
     double2 o;
     if (kind == 0) {  // arcsine law (:292-301)
       const double pi_ = pinv[i], pj_ = pinv[j];
@@ -310,11 +383,17 @@ __global__ __launch_bounds__(256) void k_gain_cr(int M, int N, const double2* __
   const double2* mu = means + (long long)k * N;
   for (int i = sl + S * tid; i < M; i += 256 * S) {
     double2 am = make_double2(0.0, 0.0);
-    for (int n = 0; n < N; ++n) am = cfma(A[(long long)i * N + n], mu[n], am);
+    if (IDA) {
+      am = mu[i];
+    } else {
+      for (int n = 0; n < N; ++n) am = cfma(A[(long long)i * N + n], mu[n], am);
+    }
     means_y[(long long)k * M + i] = cscale(am, g[i]);
   }
   for (int i = sl + S * (tid >> 6); i < M; i += 4 * S)
-    for (int n = tid & 63; n < N; n += 64) Aeff[(long long)k * M * N + (long long)i * N + n] = cscale(A[(long long)i * N + n], g[i]);
+    for (int n = tid & 63; n < N; n += 64)
+      Aeff[(long long)k * M * N + (long long)i * N + n] =
+          IDA ? make_double2(i == n ? g[i] : 0.0, 0.0) : cscale(A[(long long)i * N + n], g[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -884,12 +963,8 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
   const int K = p.K, N = p.N, M = p.M;
   hipError_t e;
   const double2 one = make_double2(1.0, 0.0), zero = make_double2(0.0, 0.0), mone = make_double2(-1.0, 0.0);
-  // Cy
-  if (p.identityA) {
-    long long total = (long long)K * N * N;
-    hipLaunchKernelGGL(k_cy_identity, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, N, total, p.covs, p.Cy,
-                       p.sigma2);
-  } else {
+  // Cy (A = I: formed inside k_gain_cr)
+  if (!p.identityA) {
     // T = A C_k (M x N), Cy = T A^H (M x M)
     if ((e = zgemm(0, 0, M, N, N, one, p.A, N, 0, p.covs, N, (long long)N * N, zero, p.work, N, (long long)M * N, K,
                    st)) != hipSuccess)
@@ -902,8 +977,14 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // row slices per component: 4 where the gains are cheap to derive in every slice (1 bit, infinite resolution)
   const unsigned gslices = (p.kind == 0 || p.kind == 2) ? 4u : 1u;
-  hipLaunchKernelGGL(k_gain_cr, dim3(K, gslices), dim3(256), (size_t)2 * M * sizeof(double), st, M, N, p.Cy, p.Cr, p.gain, p.A, p.means, p.means_y, p.Aeff,
-                     p.kind, p.n_bits, p.quant_kind, p.delta, p.thr, p.lab, p.beta_first);
+  if (p.identityA)
+    hipLaunchKernelGGL(k_gain_cr<true>, dim3(K, gslices), dim3(256), (size_t)2 * M * sizeof(double), st, M, N, p.Cy,
+                       p.Cr, p.gain, p.A, p.means, p.means_y, p.Aeff, p.kind, p.n_bits, p.quant_kind, p.delta, p.thr,
+                       p.lab, p.beta_first, p.covs, p.sigma2);
+  else
+    hipLaunchKernelGGL(k_gain_cr<false>, dim3(K, gslices), dim3(256), (size_t)2 * M * sizeof(double), st, M, N, p.Cy,
+                       p.Cr, p.gain, p.A, p.means, p.means_y, p.Aeff, p.kind, p.n_bits, p.quant_kind, p.delta, p.thr,
+                       p.lab, p.beta_first, p.covs, 0.0);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // M <= 64: QCE_CHOL = lds (default) | tri | wave picks the factorisation kernel (A/B runs; metric config,
   // rocprof: lds 116 us, tri<64> 144 us, one-wave 187 us per prepare of 128 components)
@@ -952,6 +1033,11 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
     hipLaunchKernelGGL(k_chol_inv, dim3(K), dim3(256), 0, st, M, p.Lw, p.Linv, p.logw, p.cconst, p.status);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (p.identityA && M <= 64) {
+    // V and W in one kernel (A = I)
+    hipLaunchKernelGGL(k_filter_id, dim3((M + 15) / 16, K), dim3(256), 0, st, M, p.covs, p.Linv, p.gain, p.V, p.W);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  } else {
   // X = Linv Aeff (M x N) -> work; with A = I, Aeff = diag(gain): a column scaling of Linv
   if (p.identityA) {
     const long long total = (long long)K * M * M;
@@ -970,6 +1056,7 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
   if ((e = zgemm(0, 0, N, M, M, one, p.V, M, (long long)N * M, p.Linv, M, (long long)M * M, zero, p.W, M,
                  (long long)N * M, K, st)) != hipSuccess)
     return e;
+  }
   // q0 = Linv mu_y (M x 1);  b = mu - V q0 (N x 1).  Zero-mean models: both are zero for every SNR -- the C-ABI
   // layer zero-fills them once per buffer (qce_capi.hip prepare) and the three launches are skipped
   if (p.has_mean) {

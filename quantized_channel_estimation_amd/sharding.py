@@ -144,6 +144,7 @@ class ComponentShardEstimator:
 
     native = None  # the library's K-shard step (a _lib.KShard) when built with a communicator
     _native_rows = None
+    _idx_cache = None  # {(row ranges, device): global row indices} of the last layout
 
     def __init__(self, means_cplx, covs_cplx, weights, rank, world, device=0, group=None, precision="f64", comm=None,
                  double_buffer=False):
@@ -343,8 +344,14 @@ class ComponentShardEstimator:
         ranges, h = self.native.estimate(y, mode, param, chunks=ch, scatter=scatter, stream=stream)
         idx = None
         if scatter:
-            idx = torch.cat([torch.arange(a, b, device=y.device) for a, b in ranges]) if ranges else \
-                torch.empty(0, dtype=torch.int64, device=y.device)
+            # the rows' global indices depend only on the layout: built once per layout, not per step (an arange and
+            # a cat on the compute stream between two partial kernels)
+            key = (tuple(ranges), y.device)
+            idx = self._idx_cache.get(key) if self._idx_cache else None
+            if idx is None:
+                idx = torch.cat([torch.arange(a, b, device=y.device) for a, b in ranges]) if ranges else \
+                    torch.empty(0, dtype=torch.int64, device=y.device)
+                self._idx_cache = {key: idx}
         self._native_rows = (idx, h)
         if sync:
             return self.finish()

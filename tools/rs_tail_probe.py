@@ -13,7 +13,8 @@ os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
 os.environ.setdefault("MASTER_PORT", "29561")
 torch.cuda.set_device(0)
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
-for count in (325130, 325120, 325121, 325122, 325126, 1000, 1002, 1006, 1010, 16, 18, 26):
+counts = [int(c) for c in sys.argv[1:]] or [325130, 325120, 325121, 325122, 325126, 1000, 1002, 1006, 1010, 16, 18, 26]
+for count in counts:
     for opname in ("sum", "premul", "premul_t"):
         x = torch.arange(1, count + 1, dtype=torch.float64, device="cuda")
         out = torch.zeros(count, dtype=torch.float64, device="cuda")
