@@ -316,6 +316,12 @@ def f64g_executed_flops(N, K, B, has_mean=False):
     """Executed v_mfma_f64_16x16x4 work of k_est_all_f64g (3M): per component and 16 samples 6 MFMAs per unit of two
     k-steps and 16-row tile -- GL: 2T + 2 units for tile T (the 16-row triangle), GW: MP / 8 units per tile -- plus
     2 per tile for the mean / bias columns; 2048 flops per MFMA over 16 samples."""
+    if N > 64:
+        # k_est_all_f64h (padded 128, row halves): per half 3 blocks per GL unit (36 units; + a 3-block mean unit per
+        # tile with means) and 192 GW blocks (+ 4 bias blocks), two MFMAs per block
+        hm = 1 if has_mean else 0
+        mf = 2 * (2 * 3 * (36 + 4 * hm) + 2 * (192 + 4 * hm))
+        return 2048.0 / 16.0 * mf * K * B
     Np = 16 if N <= 16 else (32 if N <= 32 else 64)
     ntl = ntw = Np // 16
     mf = 6 * sum(2 * t + 2 for t in range(ntl)) + 6 * (Np // 8) * ntw + (2 * (ntl + ntw) if has_mean else 0)
@@ -366,7 +372,8 @@ def roofline_line(args, cfg, dm, k_local, B, kern_ms, traffic):
         if N > 128:
             kernel = "k_lp_f64 + k_wsum_weights + k_wsum_f64"
         else:
-            kernel = ("k_est_all_f64g (3M)" if g3 else "k_est_all_f64") + " (+k_merge_f64)"
+            kernel = (("k_est_all_f64h (3M, row halves)" if N > 64 else "k_est_all_f64g (3M)") if g3
+                      else "k_est_all_f64") + " (+k_merge_f64)"
         line = dict(bound="mfma", achieved=round(achieved, 3), peak=FP64_MFMA_PEAK_TFLOPS, unit="TFLOP/s",
                     frac=round(frac, 4), traffic=traffic, kernel=kernel, peak_dtype="fp64 MFMA (dense)",
                     kernel_ms=round(kern_ms, 4), complex_product="3M (Gauss)" if g3 else "4M",

@@ -14,7 +14,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(config, launches, out_path, mean=False):
+def child(config, launches, out_path, mean=False, components=0):
     sys.path.insert(0, ROOT)
     import torch
     from bench import CONFIGS, make_inputs
@@ -23,6 +23,8 @@ def child(config, launches, out_path, mean=False):
     if cfg.pop("dense", False):
         os.environ["QCE_FFT"] = "0"
     cfg["mean"] = mean  # as bench.py --mean
+    if components:
+        cfg["K"] = components  # as bench.py --components (a K-shard rank's share)
     means, covs, w, h, y, qz = make_inputs(cfg, 0)
     dev = torch.device("cuda", 0)
     st = torch.cuda.Stream(dev)
@@ -55,10 +57,11 @@ def main():
     ap.add_argument("--launches", type=int, default=10)
     ap.add_argument("--child", default=None)
     ap.add_argument("--mean", action="store_true", help="components with means (as bench.py --mean)")
+    ap.add_argument("--components", type=int, default=0, help="K override (as bench.py --components)")
     ap.add_argument("variants", nargs="*")
     a = ap.parse_args()
     if a.child:
-        return child(a.config, a.launches, a.child, a.mean)
+        return child(a.config, a.launches, a.child, a.mean, a.components)
     res = {}
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     for rnd in range(a.rounds):
@@ -67,7 +70,8 @@ def main():
             env = dict(os.environ, QCE_LIB=os.path.abspath(os.path.join(ROOT, lib)))
             outp = os.path.join(ROOT, "gpurun_out", f"ab_{name}.npy")
             p = subprocess.run([sys.executable, os.path.abspath(__file__), "--config", a.config, "--launches",
-                                str(a.launches), "--child", outp] + (["--mean"] if a.mean else []), env=env, capture_output=True, text=True,
+                                str(a.launches), "--child", outp] + (["--mean"] if a.mean else []) +
+                               (["--components", str(a.components)] if a.components else []), env=env, capture_output=True, text=True,
                                timeout=300)
             if p.returncode != 0:
                 print(json.dumps({"variant": name, "error": p.stderr[-2000:]}), flush=True)
