@@ -118,12 +118,15 @@ std::vector<Chunk> chunk_layout(long long B, int chunks, int world, int rank, bo
   return out;
 }
 
-// CUs the shard's persistent estimate kernels leave free for the step's RCCL kernels (QCE_KSHARD_RESERVE_CUS,
-// default 16 = two per XCD): the grid otherwise holds every CU with one 144 KB-LDS, full-VGPR workgroup, so a
-// reduce-scatter of step t could not start before step t+1's kernel ended; with the reservation it runs beside it
+// CUs the shard's persistent estimate kernels leave free for other streams (QCE_KSHARD_RESERVE_CUS, default 0).
+// Round 6 measured that free CUs beside the persistent grid do not buy overlap: the dispatcher places a kernel's
+// workgroups on the shader engines in order and a workgroup whose engine has no free CU blocks the ones behind it, so
+// a kernel with more than ~2 workgroups per XCD (the prepare's, the row scaling, RCCL's channels) waits for the
+// persistent grid to retire anyway (tools/probe/overlap_probe.hip, profiles/r06_overlap_probe*.jsonl), while the
+// grid itself loses reserve / 256 of its CUs (emulated world-8 rank step, K = 16: 1.12 ms at 0, 1.16 ms at 16)
 int kshard_reserve_cus() {
   const char* e = getenv("QCE_KSHARD_RESERVE_CUS");
-  const int v = e ? atoi(e) : 16;
+  const int v = e ? atoi(e) : 0;
   return v < 0 ? 0 : v;
 }
 

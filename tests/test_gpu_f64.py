@@ -267,7 +267,7 @@ def test_f64_3m_matches_4m_and_oracle(N, M_pilots, mean, monkeypatch):
 
 
 def test_reserved_cus_same_estimate():
-    """QCE_OPT_RESERVE_CUS (set by the K-shard step at world > 1 so the reduce-scatter kernels find free CUs): the
+    """QCE_OPT_RESERVE_CUS (the K-shard step's QCE_KSHARD_RESERVE_CUS, default 0 since round 6): the
     persistent grid shrinks, the estimate is the same FP64 computation (1e-12; the stream-K split differs)."""
     _gpu_or_skip()
     from quantized_channel_estimation_amd import _lib

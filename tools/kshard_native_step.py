@@ -34,7 +34,7 @@ def main():
     ap.add_argument("--single-buffer", action="store_true", help="no spare table set (prepare not overlapped)")
     ap.add_argument("--reserve", type=int, default=-1,
                     help="CUs the shard's grid leaves free (QCE_OPT_RESERVE_CUS; default: the library's K-shard "
-                         "default, 16 at world > 1 or an emulated world)")
+                         "default, QCE_KSHARD_RESERVE_CUS or 0)")
     ap.add_argument("--emulate-world", default="", help="W[:R]: rehearse rank R of a W-GPU step on this world-1 rank")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-close", action="store_true", help="exit without closing the K-shard / communicator")
