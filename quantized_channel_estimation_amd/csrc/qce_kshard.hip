@@ -365,6 +365,7 @@ struct qce_kshard {
   int cur = 0;
   hipStream_t ps = nullptr;
   hipEvent_t ev_prep[2] = {nullptr, nullptr}, ev_used[2] = {nullptr, nullptr};
+  hipEvent_t ev_shift_rd[2] = {nullptr, nullptr};  // on cs: step t's read of set [i]'s shift slot (agree_shift)
   int used_valid[2] = {0, 0};
   qce_comm* c = nullptr;
   int K = 0, lo = 0, hi = 0, Kmax = 0;
@@ -613,6 +614,7 @@ int agree_shift(qce_kshard* ks, hipStream_t st) {
   KS_HIP(hipGetLastError());
   KS_HIP(hipEventRecord(ks->ev_shift_read, ks->cs));
   ks->shift_read_valid = 1;
+  if (ks->mods[1]) KS_HIP(hipEventRecord(ks->ev_shift_rd[ks->cur], ks->cs));
   KS_RC(collective(ks->c, QCE_COLL_ALLREDUCE_MAX, sh + 1, sh + 1, 1, ks->cs));
   double bias = 0.0;
   if (const char* b = getenv("QCE_KSHARD_GLOBAL_BIAS")) bias = atof(b);  // tests only
@@ -940,6 +942,7 @@ int qce_kshard_destroy(qce_kshard* ks) {
     if (ks->ev_pk[i]) (void)hipEventDestroy(ks->ev_pk[i]);
     if (ks->ev_prep[i]) (void)hipEventDestroy(ks->ev_prep[i]);
     if (ks->ev_used[i]) (void)hipEventDestroy(ks->ev_used[i]);
+    if (ks->ev_shift_rd[i]) (void)hipEventDestroy(ks->ev_shift_rd[i]);
   }
   if (ks->ps) {
     (void)hipStreamSynchronize(ks->ps);
@@ -962,7 +965,10 @@ int qce_kshard_prepare(qce_kshard* ks, const double* A, int M, double snr_db, do
   const int j = dbl ? 1 - ks->cur : 0;
   qce_model* m = ks->mods[j];
   hipStream_t ps = dbl ? ks->ps : st;
-  if (dbl && ks->used_valid[j]) KS_HIP(hipStreamWaitEvent(ps, ks->ev_used[j], 0));
+  if (dbl && ks->used_valid[j]) {
+    KS_HIP(hipStreamWaitEvent(ps, ks->ev_used[j], 0));
+    KS_HIP(hipStreamWaitEvent(ps, ks->ev_shift_rd[j], 0));
+  }
   // one table set: its shift slot is read on the communication stream at the start of each step (agree_shift), which
   // may lag behind the compute stream; the prepare that rewrites it waits for that read
   if (!dbl && ks->shift_read_valid) KS_HIP(hipStreamWaitEvent(ps, ks->ev_shift_read, 0));
@@ -999,6 +1005,7 @@ int qce_kshard_set_spare(qce_kshard* ks, qce_model* spare) {
   for (int i = 0; i < 2; ++i) {
     KS_HIP(hipEventCreateWithFlags(&ks->ev_prep[i], hipEventDisableTiming));
     KS_HIP(hipEventCreateWithFlags(&ks->ev_used[i], hipEventDisableTiming));
+    KS_HIP(hipEventCreateWithFlags(&ks->ev_shift_rd[i], hipEventDisableTiming));
   }
   ks->mods[1] = spare;
   return QCE_OK;
@@ -1041,12 +1048,16 @@ int qce_kshard_estimate(qce_kshard* ks, const double* y, int64_t B, int mode, do
       KS_RC(step_select(ks, yd, B, mode, mode_param, scatter != 0, hd, st));
     }
   }
-  KS_RC(st_to_cs(ks, st));  // the flag word closes the step behind its last kernel
-  KS_RC(close_step(ks));
-  if (dbl) {  // the table set's last readers (the step's kernels and its shift on cs): the next prepare into it waits
-    KS_HIP(hipEventRecord(ks->ev_used[ks->cur], ks->cs));
+  // the table set's readers are the step's kernels on st and the read of its shift slot on cs (ev_shift_rd): the
+  // next prepare into the set waits for those two only, not for the step's collectives and row finalisation
+  // (round 5 waited for the step's close on cs; emulated world-8 rank step 1.107 / 1.103 -> 1.080 / 1.097 ms,
+  // profiles/r06_kshard_prepare_order_ab.jsonl)
+  if (dbl) {
+    KS_HIP(hipEventRecord(ks->ev_used[ks->cur], st));
     ks->used_valid[ks->cur] = 1;
   }
+  KS_RC(st_to_cs(ks, st));  // the flag word closes the step behind its last kernel
+  KS_RC(close_step(ks));
   ks->pending.valid = 1;
   ks->pending.y = yd;
   ks->pending.B = B;

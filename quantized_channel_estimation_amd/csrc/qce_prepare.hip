@@ -1010,6 +1010,8 @@ hipError_t qce_launch_prepare(const QcePrepareArgs& p, hipStream_t st) {
       return !(e && e[0] == '0');
     }();
     const bool pairs = pairs_env && M >= 16;
+    // (round 6 tried the pair step as two barrier phases with 2 x 2-blocked rank-2 updates: tables within 2.3e-15,
+    // but every prepare 6-13 us slower -- the phases are latency-bound; profiles/r06_chol_two_phase_blocked_ab.jsonl)
     if (pairs && nt == 1024)
       hipLaunchKernelGGL(k_chol_inv_lds2<1024>, dim3(K), dim3(1024), 0, st, M, p.Cr, p.Linv, p.logw, p.cconst, p.status);
     else if (pairs && nt == 512)

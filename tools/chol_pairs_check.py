@@ -1,6 +1,7 @@
 """One-column vs two-column-per-phase Cholesky (QCE_CHOL_PAIRS) on the same models: the prepared tables
 (P = Linv^H, cconst, W, b) must be bit-identical, and the prepare time of each (HIP events, median of 20).  Each variant in its
-own process (the switch is read once per process).  python tools/chol_pairs_check.py"""
+own process (the switch is read once per process).  python tools/chol_pairs_check.py [--env QCE_CHOL_V3]: any
+on/off switch of the factorisation (variant "1" vs "0"; the tables then agree to rounding, max_rel_dev)."""
 import json
 import os
 import subprocess
@@ -9,7 +10,8 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CASES = [("metric", 128, 64), ("cfg2", 64, 64), ("cfg1", 16, 32), ("odd33", 24, 33), ("odd7", 9, 7), ("one", 3, 1)]
+CASES = [("metric", 128, 64), ("cfg2", 64, 64), ("k16", 16, 64), ("cfg1", 16, 32), ("odd33", 24, 33), ("n63", 8, 63),
+         ("odd17", 5, 17), ("odd7", 9, 7), ("one", 3, 1)]
 
 
 def child(out):
@@ -40,13 +42,14 @@ def child(out):
 
 
 def main():
-    if len(sys.argv) > 1:
+    if len(sys.argv) > 1 and sys.argv[1] != "--env":
         return child(sys.argv[1])
+    env_name = sys.argv[2] if len(sys.argv) > 2 else "QCE_CHOL_PAIRS"
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     times = {}
     for var in ("1", "0"):
         out = os.path.join(ROOT, "gpurun_out", f"chol_pairs{var}")
-        p = subprocess.run([sys.executable, os.path.abspath(__file__), out], env=dict(os.environ, QCE_CHOL_PAIRS=var),
+        p = subprocess.run([sys.executable, os.path.abspath(__file__), out], env=dict(os.environ, **{env_name: var}),
                            capture_output=True, text=True, timeout=300)
         if p.returncode:
             print(p.stderr[-3000:])
@@ -57,8 +60,8 @@ def main():
         b = np.load(os.path.join(ROOT, "gpurun_out", f"chol_pairs0_{name}.npz"))
         same = all(np.array_equal(a[k], b[k]) for k in a.files)
         dev = max(float(np.max(np.abs(a[k] - b[k])) / max(np.max(np.abs(b[k])), 1e-300)) for k in a.files)
-        print(json.dumps({"case": name, "K": K, "M": N, "bit_identical": same, "max_rel_dev": dev,
-                          "prepare_ms_pairs": times["1"][name], "prepare_ms_single": times["0"][name]}))
+        print(json.dumps({"switch": env_name, "case": name, "K": K, "M": N, "bit_identical": same, "max_rel_dev": dev,
+                          "prepare_ms_on": times["1"][name], "prepare_ms_off": times["0"][name]}))
 
 
 if __name__ == "__main__":

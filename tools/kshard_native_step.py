@@ -71,9 +71,16 @@ def main():
     torch.cuda.synchronize()
     est.native.timing(True)
     t0 = time.perf_counter()
+    hp_ms, he_ms = [], []  # host time of each prepare / estimate call (the calls are asynchronous)
     for _ in range(a.steps):
+        c0 = time.perf_counter()
         est.prepare(None, 5.0, 1)
+        c1 = time.perf_counter()
         est.estimate(yd, chunks=a.chunks, scatter=True, sync=False)
+        c2 = time.perf_counter()
+        hp_ms.append((c1 - c0) * 1e3)
+        he_ms.append((c2 - c1) * 1e3)
+    t_sub = time.perf_counter()
     rows, hk = est.finish()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
@@ -83,7 +90,9 @@ def main():
     rec = dict(kind=a.kind, double_buffer=not a.single_buffer, K=a.K, N=a.N, B=a.B, chunks=a.chunks,
                reserve_cus=a.reserve, emulate_world=a.emulate_world or None, rows=int(r.size), steps=a.steps,
                ms_per_step=dt * 1e3, partial_kernel_ms_per_step=kms / a.steps, launches=nl,
-               est_per_s_rank_rows=r.size / dt)
+               est_per_s_rank_rows=r.size / dt, host_submit_ms_per_step=(t_sub - t0) * 1e3 / a.steps,
+               host_prepare_ms=[round(float(np.median(hp_ms)), 4), round(max(hp_ms), 4)],
+               host_estimate_ms=[round(float(np.median(he_ms)), 4), round(max(he_ms), 4)])
     if not a.no_parity:
         from oracle import qce_oracle as O
         ho = O.estimate(means, covs, w, y[r[:512]], 5.0, a.N, None, "all", 1)
