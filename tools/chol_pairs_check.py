@@ -4,8 +4,10 @@ own process (the switch is read once per process).  python tools/chol_pairs_chec
 on/off switch of the factorisation (variant "1" vs "0"; the tables then agree to rounding, max_rel_dev)."""
 import json
 import os
+import shutil
 import subprocess
 import sys
+import tempfile
 
 import numpy as np
 
@@ -34,7 +36,7 @@ def child(out):
             e1.record(st)
             torch.cuda.synchronize()
             ts.append(e0.elapsed_time(e1))
-        t = dm.tables(["P", "cconst", "W", "b"])
+        t = dm.tables(["means_y", "Cy", "Cr", "P", "A_eff", "W", "b", "cconst"])
         np.savez(out + f"_{name}.npz", **{k: np.asarray(v) for k, v in t.items()})
         res[name] = float(np.median(ts))
         dm.close()
@@ -45,10 +47,10 @@ def main():
     if len(sys.argv) > 1 and sys.argv[1] != "--env":
         return child(sys.argv[1])
     env_name = sys.argv[2] if len(sys.argv) > 2 else "QCE_CHOL_PAIRS"
-    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    scratch = tempfile.mkdtemp(prefix="qce_chol_check_")  # the table dumps (tens of MB) stay off gpurun_out
     times = {}
     for var in ("1", "0"):
-        out = os.path.join(ROOT, "gpurun_out", f"chol_pairs{var}")
+        out = os.path.join(scratch, f"chol_pairs{var}")
         p = subprocess.run([sys.executable, os.path.abspath(__file__), out], env=dict(os.environ, **{env_name: var}),
                            capture_output=True, text=True, timeout=300)
         if p.returncode:
@@ -56,12 +58,13 @@ def main():
             return 1
         times[var] = json.loads(p.stdout.strip().splitlines()[-1])
     for name, K, N in CASES:
-        a = np.load(os.path.join(ROOT, "gpurun_out", f"chol_pairs1_{name}.npz"))
-        b = np.load(os.path.join(ROOT, "gpurun_out", f"chol_pairs0_{name}.npz"))
+        a = np.load(os.path.join(scratch, f"chol_pairs1_{name}.npz"))
+        b = np.load(os.path.join(scratch, f"chol_pairs0_{name}.npz"))
         same = all(np.array_equal(a[k], b[k]) for k in a.files)
         dev = max(float(np.max(np.abs(a[k] - b[k])) / max(np.max(np.abs(b[k])), 1e-300)) for k in a.files)
         print(json.dumps({"switch": env_name, "case": name, "K": K, "M": N, "bit_identical": same, "max_rel_dev": dev,
                           "prepare_ms_on": times["1"][name], "prepare_ms_off": times["0"][name]}))
+    shutil.rmtree(scratch, ignore_errors=True)
 
 
 if __name__ == "__main__":
