@@ -168,6 +168,18 @@ unsigned grid_for(long long n) {
   return (unsigned)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
 }
 
+// the row passes that run beside the next prepare (the send rows' scaling, the finalisation): their grid capped at
+// QCE_KSHARD_ROWPASS_WG workgroups (grid-stride), so they do not queue thousands of workgroups ahead of the prepare's
+// kernels in the dispatcher (A/B knob; 0 or unset = grid_for)
+unsigned rowpass_grid(long long n) {
+  static const long cap = [] {
+    const char* e = getenv("QCE_KSHARD_ROWPASS_WG");
+    return e ? atol(e) : 0L;
+  }();
+  const unsigned g = grid_for(n);
+  return (cap > 0 && (long)g > cap) ? (unsigned)cap : g;
+}
+
 // h[r] = acc[r] / s[r] from packed rows [s, 0, acc (2N)]; rows with s below the normal range are counted
 __global__ __launch_bounds__(256) void k_ks_finalize(long long n, int N, const double* __restrict__ rows,
                                                      double2* __restrict__ h, double thr, unsigned* __restrict__ cnt) {
@@ -241,6 +253,16 @@ __global__ void k_ks_spin(long long ticks) {
 __global__ __launch_bounds__(256) void k_ks_scale_rows(long long n, double* __restrict__ v,
                                                        const double* __restrict__ sc) {
   const double f = *sc;
+  if ((reinterpret_cast<uintptr_t>(v) & 15) == 0) {  // 16-byte accesses, then the odd last element
+    double2* v2 = reinterpret_cast<double2*>(v);
+    const long long n2 = n >> 1;
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n2; i += (long long)gridDim.x * 256) {
+      const double2 a = v2[i];
+      v2[i] = make_double2(a.x * f, a.y * f);
+    }
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) v[n - 1] *= f;
+    return;
+  }
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) v[i] *= f;
 }
 
@@ -543,7 +565,7 @@ int reduce_chunks(qce_kshard* ks, const std::vector<Chunk>& L, bool scatter, int
     // RCCL the chunk's rows -- every row this rank contributes -- are therefore scaled by a kernel first and the
     // reduce-scatter is a plain SUM.
     if (premul && c->kind == QCE_COMM_RCCL) {
-      hipLaunchKernelGGL(k_ks_scale_rows, dim3(grid_for(ch.npad * W)), dim3(256), 0, ks->cs, ch.npad * W, send, premul);
+      hipLaunchKernelGGL(k_ks_scale_rows, dim3(rowpass_grid(ch.npad * W)), dim3(256), 0, ks->cs, ch.npad * W, send, premul);
       KS_HIP(hipGetLastError());
       premul = nullptr;
     }
@@ -557,7 +579,7 @@ int reduce_chunks(qce_kshard* ks, const std::vector<Chunk>& L, bool scatter, int
     rows = send;
   }
   if (ch.nv > 0) {
-    hipLaunchKernelGGL(k_ks_finalize, dim3(grid_for(ch.nv * N)), dim3(256), 0, ks->cs, ch.nv, N, rows,
+    hipLaunchKernelGGL(k_ks_finalize, dim3(rowpass_grid(ch.nv * N)), dim3(256), 0, ks->cs, ch.nv, N, rows,
                        h_out + ch.h_off * N, count_flags ? kUnderflowS : -1.0, ks->cnt.p);
     KS_HIP(hipGetLastError());
   }
