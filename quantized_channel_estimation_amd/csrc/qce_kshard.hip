@@ -392,6 +392,8 @@ struct qce_kshard {
   qce_comm* c = nullptr;
   int K = 0, lo = 0, hi = 0, Kmax = 0;
   int lw = 1, lr = 0;  // world / rank the rows are laid out for: the communicator's, or QCE_KSHARD_EMULATE_WORLD's
+  int agree_first = 0;  // 'all' mode: M* agreed before the partial kernel, which then writes rows shifted by M*
+                        // (no scaling pass; QCE_KSHARD_AGREE_FIRST); 2: world-1 probe that skips the scaling only
   int reserve = 0;     // CUs the step's persistent kernels leave to the communication stream (unless the caller set
                        // QCE_OPT_RESERVE_CUS on the model; applied per launch, the model is not modified)
   hipStream_t cs = nullptr;  // communication stream: the chunks' collectives and row finalisation
@@ -693,14 +695,17 @@ int step_all(qce_kshard* ks, qce_model* m, const double2* y, long long B, int ch
         KS_RC(timed_begin(ks, st));
         ReserveScope rsv(m, ks->reserve);
         // the shard's own shift M_r, read straight from the table set's slot (final once st waited for its prepare)
-        ok = guarded(ks, qce_estimate_partial_shifted(m, reinterpret_cast<const double*>(y + ch.lo * M), n,
-                                                      ks->shift.p + ks->cur, pk, QCE_IO_DEVICE, st), &hard);
+        // agree-first: the agreed M* (the compute stream waited for the MAX), so the rows enter the SUM unscaled
+        const double* shp = ks->agree_first == 1 ? ks->step_shift.p + 2 * ks->pkp + 1 : ks->shift.p + ks->cur;
+        ok = guarded(ks, qce_estimate_partial_shifted(m, reinterpret_cast<const double*>(y + ch.lo * M), n, shp, pk,
+                                                      QCE_IO_DEVICE, st), &hard);
         if (hard) return hard;
         KS_RC(timed_end(ks, st));
       }
       if (!ok) KS_HIP(hipMemsetAsync(pk, 0, sizeof(double) * n * W, st));
     }
-    KS_RC(reduce_chunks(ks, L, scatter, W, st, h, !rowshift, i, rowshift ? nullptr : ks->scale.p + ks->pkp));
+    KS_RC(reduce_chunks(ks, L, scatter, W, st, h, !rowshift, i,
+                        (rowshift || ks->agree_first) ? nullptr : ks->scale.p + ks->pkp));
   }
   return QCE_OK;
 }
@@ -911,6 +916,11 @@ int qce_kshard_create(qce_model* shard, qce_comm* comm, int K_total, qce_kshard*
   ks->lr = comm->rank;
   if (comm->world == 1) (void)kshard_emulated(&ks->lw, &ks->lr);
   if (comm->kind == QCE_COMM_RCCL && ks->lw > 1) ks->reserve = kshard_reserve_cus();
+  if (const char* af = getenv("QCE_KSHARD_AGREE_FIRST")) {
+    ks->agree_first = atoi(af);
+    // the probe (2) leaves the rows unscaled: exact only where M* = M_r, i.e. one real rank
+    if (ks->agree_first == 2 && comm->world != 1) ks->agree_first = 0;
+  }
   ks->m = shard;
   ks->mods[0] = shard;
   ks->device = shard->device;
@@ -1063,6 +1073,7 @@ int qce_kshard_estimate(qce_kshard* ks, const double* y, int64_t B, int mode, do
     KS_HIP(hipGetLastError());
   }
   KS_RC(agree_shift(ks, st));
+  if (ks->agree_first == 1 && mode == QCE_MODE_ALL && B > 0) KS_RC(cs_to_st(ks, st));  // the partial reads M*
   if (B > 0) {
     if (mode == QCE_MODE_ALL) {
       KS_RC(step_all(ks, ks->m, yd, B, chunks, scatter != 0, hd, st, false));

@@ -45,15 +45,18 @@ def _metric_batch(K, N, B, seed=77):
     return means, covs, w, y
 
 
-@pytest.mark.parametrize("world,rank,chunks", [(8, 0, 1), (8, 5, 1), (4, 3, 2), (8, 7, 1)])
-def test_emulated_world_rank_rows_equal_single_gpu(rccl1, monkeypatch, world, rank, chunks):
+@pytest.mark.parametrize("world,rank,chunks,agree_first", [(8, 0, 1, 0), (8, 5, 1, 0), (4, 3, 2, 0), (8, 7, 1, 0),
+                                                            (8, 3, 1, 1), (4, 1, 2, 1)])
+def test_emulated_world_rank_rows_equal_single_gpu(rccl1, monkeypatch, world, rank, chunks, agree_first):
     """Rank `rank` of an emulated `world`-GPU step (K = 16 components per rank at the metric's N = 64, B = 20001 so
     the last chunk is ragged): the rows returned are exactly the rank's reduce-scatter slice and equal the single-GPU
-    estimate of the same mixture to 1e-12."""
+    estimate of the same mixture to 1e-12.  agree_first = 1: the shift MAX before the partial kernel, rows written
+    shifted by the agreed M* and summed unscaled (QCE_KSHARD_AGREE_FIRST, the A/B alternative to the scaling pass)."""
     import torch
     from quantized_channel_estimation_amd import _lib
     from quantized_channel_estimation_amd.sharding import ComponentShardEstimator, chunk_bounds
     monkeypatch.setenv("QCE_KSHARD_EMULATE_WORLD", f"{world}:{rank}")
+    monkeypatch.setenv("QCE_KSHARD_AGREE_FIRST", str(agree_first))
     K, N, B = 16, 64, 20001
     means, covs, w, y = _metric_batch(K, N, B)
     est = ComponentShardEstimator(means, covs, w, 0, 1, device=0, comm=rccl1, double_buffer=True)
