@@ -266,6 +266,25 @@ __global__ __launch_bounds__(256) void k_ks_scale_rows(long long n, double* __re
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) v[i] *= f;
 }
 
+// one-time check of RCCL's PreMulSum reduce-scatter at a given count (see reduce_chunks): send[j] = j mod P + 1 on
+// every rank, scalar 0.5 in pr[0]; rank r's slice must come back as world * 0.5 * (send value at r count + i)
+constexpr long long kProbeP = 1048573;
+__global__ __launch_bounds__(256) void k_ks_probe_fill(double* __restrict__ send, long long n, double* __restrict__ pr) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    pr[0] = 0.5;
+    pr[1] = 0.0;
+  }
+  for (long long j = (long long)blockIdx.x * 256 + threadIdx.x; j < n; j += (long long)gridDim.x * 256)
+    send[j] = (double)(j % kProbeP + 1);
+}
+__global__ __launch_bounds__(256) void k_ks_probe_check(const double* __restrict__ recv, long long count, int world,
+                                                        int rank, double* __restrict__ bad) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < count; i += (long long)gridDim.x * 256) {
+    const double want = world * 0.5 * (double)(((long long)rank * count + i) % kProbeP + 1);
+    if (recv[i] != want) *bad = 1.0;  // every writer stores the same value
+  }
+}
+
 // first maximum of each lp row (numpy argmax) as (value, index) doubles, one wave per row
 __global__ __launch_bounds__(256) void k_ks_row_argmax(long long B, int K, const double* __restrict__ lp,
                                                        double* __restrict__ out) {
@@ -405,6 +424,8 @@ struct qce_kshard {
   KBuf<double> step_shift;              // [2 parity + 0]: the shard's shift M_r the step's kernels used (copied on the
                                         // compute stream); [2 parity + 1]: the agreed M* (MAX on the comm stream)
   KBuf<double> scale;                   // [parity]: e^{M_r - M*}, the PreMulSum scalar of the step's SUMs
+  KBuf<double> probe;                   // PreMulSum reduce-scatter check: [scalar, mismatch flag]
+  std::vector<std::pair<long long, int>> rs_premul;  // (count, RCCL's PreMulSum reduce-scatter exact at that count)
   hipEvent_t ev_pk[2] = {nullptr, nullptr};  // recorded on cs after the last reader of pkb[p] / step_shift[p]
   int pk_valid[2] = {0, 0};
   hipEvent_t ev_st2cs = nullptr, ev_cs2st = nullptr;
@@ -547,6 +568,42 @@ int timed_end(qce_kshard* ks, hipStream_t st) {
   return QCE_OK;
 }
 
+// RCCL's PreMulSum reduce-scatter at `count` doubles per rank: exact (1) or not (0), from the cache or, the first
+// time a count is used, from one check run in the step's own buffers (before any partial kernel of the step is
+// enqueued: the host waits for it) and agreed over the ranks with a MAX, so every rank takes the same path.
+int rs_premul_exact(qce_kshard* ks, double* send, double* recv, long long count, int* ok) {
+  for (const auto& e : ks->rs_premul)
+    if (e.first == count) {
+      *ok = e.second;
+      return QCE_OK;
+    }
+  qce_comm* c = ks->c;
+  KS_HIP(ks->probe.ensure(2));
+  const long long n = count * c->world;
+  hipLaunchKernelGGL(k_ks_probe_fill, dim3(grid_for(n)), dim3(256), 0, ks->cs, send, n, ks->probe.p);
+  KS_HIP(hipGetLastError());
+  KS_RC(collective(c, QCE_COLL_REDUCE_SCATTER_SUM, send, recv, count, ks->cs, ks->probe.p));
+  hipLaunchKernelGGL(k_ks_probe_check, dim3(grid_for(count)), dim3(256), 0, ks->cs, recv, count, c->world, c->rank,
+                     ks->probe.p + 1);
+  KS_HIP(hipGetLastError());
+  KS_RC(collective(c, QCE_COLL_ALLREDUCE_MAX, ks->probe.p + 1, ks->probe.p + 1, 1, ks->cs));
+  double bad = 1.0;
+  KS_HIP(hipMemcpyAsync(&bad, ks->probe.p + 1, sizeof(double), hipMemcpyDeviceToHost, ks->cs));
+  KS_HIP(hipStreamSynchronize(ks->cs));
+  *ok = bad == 0.0 ? 1 : 0;
+  ks->rs_premul.emplace_back(count, *ok);
+  return QCE_OK;
+}
+
+// QCE_KSHARD_RS_PREMUL=0: never use RCCL's PreMulSum reduce-scatter (always the scaling kernel + SUM)
+bool rs_premul_allowed() {
+  static const bool on = [] {
+    const char* e = getenv("QCE_KSHARD_RS_PREMUL");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // the SUM collectives of a step's packed rows (pk, W doubles per row) per chunk on the communication stream, each
 // behind its own chunk's producer on `st`, and the rows' finalisation h = acc / s into h_out
 int reduce_chunks(qce_kshard* ks, const std::vector<Chunk>& L, bool scatter, int W, hipStream_t st, double2* h_out,
@@ -561,19 +618,29 @@ int reduce_chunks(qce_kshard* ks, const std::vector<Chunk>& L, bool scatter, int
   const double* rows;
   if (scatter) {
     const long long q = ch.npad / ks->lw;
-    // The librccl this links against (2.26.6, the one torch ships) loses the tail of a large reduce-scatter with a
+    // The librccl this links against (2.26.6, the one torch ships) loses the tail of some reduce-scatters with a
     // PreMulSum op: up to 16 doubles past a boundary that depends on the count (measured on the box,
-    // tools/rs_tail_probe.py, profiles/r06_rs_tail_probe*.jsonl; SUM, and all-reduce with PreMulSum, are exact).  Over
-    // RCCL the chunk's rows -- every row this rank contributes -- are therefore scaled by a kernel first and the
-    // reduce-scatter is a plain SUM.
-    if (premul && c->kind == QCE_COMM_RCCL) {
-      hipLaunchKernelGGL(k_ks_scale_rows, dim3(rowpass_grid(ch.npad * W)), dim3(256), 0, ks->cs, ch.npad * W, send, premul);
-      KS_HIP(hipGetLastError());
-      premul = nullptr;
-    }
+    // tools/rs_tail_probe.py, profiles/r06_rs_tail_probe*.jsonl; SUM, and all-reduce with PreMulSum, are exact).  Each
+    // count is therefore checked once on the real communicator (rs_premul_exact); at a count where the PreMulSum
+    // reduce-scatter is not exact the chunk's rows -- every row this rank contributes -- are scaled by a kernel first
+    // and the reduce-scatter is a plain SUM.
     // an emulated layout on a world-1 communicator: the rank's own q rows are the whole world-1 reduce-scatter
-    if (ks->lw != c->world) send += (long long)ks->lr * q * W;
+    double* send_rs = send + (ks->lw != c->world ? (long long)ks->lr * q * W : 0LL);
     double* recv = ks->rs.p + ch.rs_off * W;
+    if (premul && c->kind == QCE_COMM_RCCL) {
+      // the count's PreMulSum check ran before the step's partial kernels (step_all); where RCCL's PreMulSum
+      // reduce-scatter is exact the scaling rides the collective, elsewhere a kernel scales every row first
+      int ok = 0;
+      for (const auto& e : ks->rs_premul)
+        if (e.first == q * W) ok = e.second;
+      if (!ok || !rs_premul_allowed()) {
+        hipLaunchKernelGGL(k_ks_scale_rows, dim3(rowpass_grid(ch.npad * W)), dim3(256), 0, ks->cs, ch.npad * W, send,
+                           premul);
+        KS_HIP(hipGetLastError());
+        premul = nullptr;
+      }
+    }
+    send = send_rs;
     KS_RC(collective(c, QCE_COLL_REDUCE_SCATTER_SUM, send, recv, q * W, ks->cs, premul));
     rows = recv;
   } else {
@@ -663,6 +730,14 @@ int step_all(qce_kshard* ks, qce_model* m, const double2* y, long long B, int ch
   KS_HIP(pkbuf.ensure((size_t)pk_rows * W));
   if (scatter) KS_HIP(ks->rs.ensure((size_t)rs_rows * W));
   KS_RC(ensure_events(ks, L.size()));
+  if (scatter && !rowshift && !ks->agree_first && c->kind == QCE_COMM_RCCL && rs_premul_allowed()) {
+    for (const Chunk& ch : L) {  // each new count checked once, in the rows this step is about to fill
+      const long long q = ch.npad / ks->lw;
+      double* send = pkbuf.p + ch.pk_off * W + (ks->lw != c->world ? (long long)ks->lr * q * W : 0LL);
+      int ok;
+      KS_RC(rs_premul_exact(ks, send, ks->rs.p + ch.rs_off * W, q * W, &ok));
+    }
+  }
   int hard = QCE_OK;
   if (rowshift) {
     // exact recombination: m (running max), s, acc of this shard for the whole batch; mg = MAX over shards of m
@@ -956,7 +1031,7 @@ int qce_kshard_destroy(qce_kshard* ks) {
   if (!ks) return QCE_OK;
   DevGuard g(ks->device);
   if (ks->cs) (void)hipStreamSynchronize(ks->cs);
-  for (auto* b : {&ks->shift, &ks->fl, &ks->earlier, &ks->pkb[0], &ks->pkb[1], &ks->step_shift, &ks->scale, &ks->rs,
+  for (auto* b : {&ks->shift, &ks->fl, &ks->earlier, &ks->pkb[0], &ks->pkb[1], &ks->step_shift, &ks->scale, &ks->probe, &ks->rs,
                   &ks->rm, &ks->rsum, &ks->racc, &ks->mg, &ks->lp, &ks->lpad, &ks->gath, &ks->lpfull, &ks->wfull,
                   &ks->wloc})
     b->release();
